@@ -1,0 +1,122 @@
+/*
+ * kzgpot — MI355X-native Powers-of-Tau → arkworks KZG preprocessor: the C ABI.
+ *
+ * Drop-in boundary for the per-point hot path of heliaxdev/kzg-setup-powersoftau. The reference
+ * is a Rust crate with no FFI; each entry point below names the reference code it replaces
+ * (paths relative to the reference repo root). A Rust crate binds these with `extern "C"` (see
+ * INTEGRATION.md); the Python package and the tests bind them with ctypes.
+ *
+ * Conventions
+ *  - Plain pointers and sizes only. Host variants take host buffers and are synchronous. `_dev`
+ *    variants take device pointers (HBM) and a hipStream_t passed as void*; they are
+ *    asynchronous and report errors through a device-side key (see kzgpot_decode_bad_key).
+ *  - Point formats: G1 compressed 48 B / uncompressed 96 B, G2 compressed 96 B / uncompressed
+ *    192 B. "pairing" = zcash pairing 0.14.2 big-endian encodings as written by powersoftau;
+ *    "ark" = ark-serialize 0.2 `serialize_uncompressed` (little-endian, SWFlags in the top byte).
+ *  - Return value: 0 = every point accepted; -(status) of the FIRST rejected point (smallest
+ *    index, deterministic) when a point is rejected; <= KZGPOT_E_INVALID_ARG on API/runtime errors.
+ *    Rejected points' output records are zero-filled. The reference panics on the first bad point
+ *    (`unwrap`, preprocess-kgz.rs:110,142); callers that want that behaviour abort on != 0.
+ *  - Accept/reject and output bytes are bit-exact with the reference for every input; the error
+ *    CLASS is informative (the reference's own class depends on which stage trips first).
+ */
+#ifndef KZGPOT_H
+#define KZGPOT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------------------------------------------------------- per-point status / errors */
+#define KZGPOT_OK 0
+#define KZGPOT_ST_COMPRESSION_MODE 1 /* pairing GroupDecodingError::UnexpectedCompressionMode */
+#define KZGPOT_ST_UNEXPECTED_INFO 2  /* pairing GroupDecodingError::UnexpectedInformation */
+#define KZGPOT_ST_NOT_IN_FIELD 3     /* pairing CoordinateDecodingError / ark InvalidData (coord >= p) */
+#define KZGPOT_ST_NOT_ON_CURVE 4     /* pairing GroupDecodingError::NotOnCurve (x^3+b non-residue) */
+#define KZGPOT_ST_NOT_IN_SUBGROUP 5  /* ark InvalidData from is_in_correct_subgroup_assuming_on_curve */
+#define KZGPOT_ST_UNEXPECTED_FLAGS 6 /* ark SerializationError::UnexpectedFlags */
+#define KZGPOT_ST_INFINITY 7         /* point at infinity reaching read_g1/read_g2: the reference panics */
+
+#define KZGPOT_E_INVALID_ARG (-100)
+#define KZGPOT_E_DEVICE (-101)  /* HIP runtime failure or no usable GPU: the product path never falls back to CPU */
+#define KZGPOT_E_IO (-102)
+#define KZGPOT_E_SIZE (-103)    /* transcript size != powersoftau CONTRIBUTION_BYTE_SIZE (preprocess-kgz.rs:83-91) */
+#define KZGPOT_E_DIGEST (-104)  /* BLAKE2b-512 mismatch (preprocess-kgz.rs:51-61, src/lib.rs:147-157) */
+#define KZGPOT_E_NETWORK (-105) /* download requested: this build has no network client */
+
+/* ---------------------------------------------------------------- flags */
+/* Decompression only (powersoftau CheckForCorrectness::No with no read_g1 afterwards — the βτG1 /
+ * βG2 sections in preprocess-kgz). The point at infinity is then legal and is emitted as ark
+ * GroupAffine::zero(). Default (flag clear): the full reference chain of a point that is read
+ * back by read_g1/read_g2 — infinity rejected, subgroup checked. */
+#define KZGPOT_NO_SUBGROUP_CHECK 0x1u
+/* Use the reference's own subgroup algorithm (ark mul_bits by r, 255-bit double-and-add) instead
+ * of the endomorphism test. Same boolean for every point; ~3x slower. For cross-validation. */
+#define KZGPOT_SUBGROUP_REF 0x2u
+
+/* ---------------------------------------------------------------- hot path, host buffers */
+/* Compressed G1 (48 B each, pairing) → ark uncompressed (96 B each).
+ * Replaces, per point: pairing G1Compressed::into_affine_unchecked (via powersoftau
+ * Accumulator::deserialize, src/bin/preprocess-kgz.rs:105-110) → G1Uncompressed (preprocess-kgz.rs:122)
+ * → read_g1 (src/lib.rs:41-54, incl. ark subgroup check) → serialize_uncompressed (preprocess-kgz.rs:188-194). */
+int kzgpot_g1_decompress(const uint8_t* in, size_t n, uint8_t* out, uint32_t flags, int64_t* first_bad);
+/* Compressed G2 (96 B) → ark uncompressed (192 B). Same chain with read_g2 (src/lib.rs:56-80) and the
+ * fastkgz G2 emit (src/bin/preprocess-fastkgz.rs:206-208). */
+int kzgpot_g2_decompress(const uint8_t* in, size_t n, uint8_t* out, uint32_t flags, int64_t* first_bad);
+/* Pairing-uncompressed G1 (96 B) → ark (96 B): the read_g1 loop alone (src/lib.rs:41-54;
+ * preprocess-kgz.rs:140-153; load_phase1 src/lib.rs:92-110). flags: KZGPOT_SUBGROUP_REF only. */
+int kzgpot_g1_transcode_uncompressed(const uint8_t* in, size_t n, uint8_t* out, uint32_t flags, int64_t* first_bad);
+/* Pairing-uncompressed G2 (192 B) → ark (192 B): the read_g2 loop (src/lib.rs:56-80). */
+int kzgpot_g2_transcode_uncompressed(const uint8_t* in, size_t n, uint8_t* out, uint32_t flags, int64_t* first_bad);
+
+/* As above, also writing one status byte per point (KZGPOT_ST_*) into status[n] (may be NULL). */
+int kzgpot_g1_decompress_ex(const uint8_t* in, size_t n, uint8_t* out, uint32_t flags, int64_t* first_bad, uint8_t* status);
+int kzgpot_g2_decompress_ex(const uint8_t* in, size_t n, uint8_t* out, uint32_t flags, int64_t* first_bad, uint8_t* status);
+int kzgpot_g1_transcode_uncompressed_ex(const uint8_t* in, size_t n, uint8_t* out, uint32_t flags, int64_t* first_bad, uint8_t* status);
+int kzgpot_g2_transcode_uncompressed_ex(const uint8_t* in, size_t n, uint8_t* out, uint32_t flags, int64_t* first_bad, uint8_t* status);
+
+/* ---------------------------------------------------------------- hot path, device buffers (async) */
+/* d_bad_key: one device uint64 that the call resets to UINT64_MAX (on `stream`) and that the
+ * kernel lowers with atomicMin((index << 8) | status). d_status may be NULL. */
+int kzgpot_g1_decompress_dev(const void* d_in, size_t n, void* d_out, uint32_t flags, uint64_t* d_bad_key,
+                             uint8_t* d_status, void* stream);
+int kzgpot_g2_decompress_dev(const void* d_in, size_t n, void* d_out, uint32_t flags, uint64_t* d_bad_key,
+                             uint8_t* d_status, void* stream);
+int kzgpot_g1_transcode_uncompressed_dev(const void* d_in, size_t n, void* d_out, uint32_t flags,
+                                         uint64_t* d_bad_key, uint8_t* d_status, void* stream);
+int kzgpot_g2_transcode_uncompressed_dev(const void* d_in, size_t n, void* d_out, uint32_t flags,
+                                         uint64_t* d_bad_key, uint8_t* d_status, void* stream);
+/* Host-side decode of a bad key copied back from the device: returns 0 (none) or -(status) and
+ * sets *first_bad to the index (or -1). */
+int kzgpot_decode_bad_key(uint64_t key, int64_t* first_bad);
+
+/* ---------------------------------------------------------------- file pipeline (next-row §8f) */
+#define KZGPOT_MODE_KZG 0     /* src/bin/preprocess-kgz.rs: Powers + VerifierKey file */
+#define KZGPOT_MODE_FASTKZG 1 /* src/bin/preprocess-fastkgz.rs: UniversalParams + powers_of_h file */
+/* powersoftau CONTRIBUTION_BYTE_SIZE for 2^n_log2 powers (603,981,040 at n_log2 = 21). */
+uint64_t kzgpot_contribution_size(uint32_t n_log2);
+/* Output size of `mode` for 2^n_log2 powers (kgz 603,980,256 / fastkzg 1,006,633,248 at 21). */
+uint64_t kzgpot_output_size(uint32_t n_log2, int mode);
+/* preprocess-{kgz,fastkgz} main (preprocess-kgz.rs:162-199, preprocess-fastkgz.rs:180-213) minus the
+ * download: reads the response transcript at `transcript_path`, checks its size, decompresses and
+ * checks every section on n_gpus GPUs (0 = all visible), writes `out_path`. No intermediate file.
+ * Returns 0 or a negative error; on a rejected point *bad_section (0 τG1, 1 τG2, 2 ατG1, 3 βτG1,
+ * 4 βG2) and *bad_index locate it (pointers may be NULL). */
+int kzgpot_preprocess(const char* transcript_path, const char* out_path, int mode, uint32_t n_log2, int n_gpus,
+                      int* bad_section, int64_t* bad_index);
+/* Same, on in-memory buffers (out must hold kzgpot_output_size bytes). */
+int kzgpot_preprocess_buffer(const uint8_t* transcript, size_t len, uint8_t* out, int mode, uint32_t n_log2,
+                             int n_gpus, int* bad_section, int64_t* bad_index);
+
+/* ---------------------------------------------------------------- misc */
+const char* kzgpot_status_name(int status);  /* name of a KZGPOT_ST_* or KZGPOT_E_* code */
+int kzgpot_device_count(void);               /* visible HIP devices (0 if none) */
+const char* kzgpot_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KZGPOT_H */

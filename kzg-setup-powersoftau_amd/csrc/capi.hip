@@ -1,0 +1,299 @@
+// C ABI (include/kzgpot.h): host-buffer and device-buffer entry points for the point codec, and
+// the kgz / fastkzg file pipeline. No CPU fallback exists: without a GPU every entry point
+// returns KZGPOT_E_DEVICE.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "codec.hpp"
+
+using namespace kzgpot;
+
+namespace {
+
+constexpr uint64_t kNoBad = ~0ull;
+
+#define HIP_TRY(expr)                                                                    \
+  do {                                                                                   \
+    hipError_t e_ = (expr);                                                              \
+    if (e_ != hipSuccess) {                                                              \
+      fprintf(stderr, "kzgpot: %s failed: %s (%s:%d)\n", #expr, hipGetErrorString(e_), \
+              __FILE__, __LINE__);                                                       \
+      return KZGPOT_E_DEVICE;                                                            \
+    }                                                                                    \
+  } while (0)
+
+// Per-device staging buffers for the host-buffer API (grown on demand, reused across calls).
+struct DevCtx {
+  std::mutex mu;
+  hipStream_t stream = nullptr;
+  void* d_in = nullptr;
+  void* d_out = nullptr;
+  uint8_t* d_status = nullptr;
+  unsigned long long* d_key = nullptr;
+  size_t cap_in = 0, cap_out = 0, cap_status = 0;
+};
+DevCtx g_ctx[64];
+
+int ensure(void** p, size_t* cap, size_t need) {
+  if (*cap >= need) return 0;
+  if (*p) HIP_TRY(hipFree(*p));
+  *p = nullptr;
+  *cap = 0;
+  HIP_TRY(hipMalloc(p, need));
+  *cap = need;
+  return 0;
+}
+
+int device_count() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int decode_key(uint64_t key, int64_t* first_bad) {
+  if (key == kNoBad) {
+    if (first_bad) *first_bad = -1;
+    return 0;
+  }
+  if (first_bad) *first_bad = (int64_t)(key >> 8);
+  return -(int)(key & 0xff);
+}
+
+// Run one op over host buffers on device `dev`, in chunks that bound the staging memory.
+int run_host(int dev, CodecOp op, const uint8_t* in, size_t n, uint8_t* out, uint32_t flags, int64_t* first_bad,
+             uint8_t* status) {
+  if (first_bad) *first_bad = -1;
+  if (n == 0) return 0;
+  if (!in || !out) return KZGPOT_E_INVALID_ARG;
+  if (dev < 0 || dev >= device_count() || dev >= 64) return KZGPOT_E_DEVICE;
+  DevCtx& c = g_ctx[dev];
+  std::lock_guard<std::mutex> lock(c.mu);
+  HIP_TRY(hipSetDevice(dev));
+  if (!c.stream) HIP_TRY(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
+  const uint64_t rin = in_record(op), rout = out_record(op);
+  const size_t chunk = std::min<size_t>(n, (size_t)1 << 22);
+  if (ensure(&c.d_in, &c.cap_in, chunk * rin)) return KZGPOT_E_DEVICE;
+  if (ensure(&c.d_out, &c.cap_out, chunk * rout)) return KZGPOT_E_DEVICE;
+  if (ensure((void**)&c.d_status, &c.cap_status, chunk)) return KZGPOT_E_DEVICE;
+  if (!c.d_key) HIP_TRY(hipMalloc(&c.d_key, sizeof(unsigned long long)));
+  uint64_t best = kNoBad;
+  for (size_t off = 0; off < n; off += chunk) {
+    const size_t m = std::min(chunk, n - off);
+    HIP_TRY(hipMemcpyAsync(c.d_in, in + off * rin, m * rin, hipMemcpyHostToDevice, c.stream));
+    HIP_TRY(hipMemsetAsync(c.d_key, 0xff, sizeof(unsigned long long), c.stream));
+    HIP_TRY(launch_codec(op, c.d_in, c.d_out, m, flags, c.d_key, status ? c.d_status : nullptr, c.stream));
+    HIP_TRY(hipMemcpyAsync(out + off * rout, c.d_out, m * rout, hipMemcpyDeviceToHost, c.stream));
+    if (status) HIP_TRY(hipMemcpyAsync(status + off, c.d_status, m, hipMemcpyDeviceToHost, c.stream));
+    unsigned long long key = kNoBad;
+    HIP_TRY(hipMemcpyAsync(&key, c.d_key, sizeof key, hipMemcpyDeviceToHost, c.stream));
+    HIP_TRY(hipStreamSynchronize(c.stream));
+    if (key != kNoBad && best == kNoBad) best = ((uint64_t)(key >> 8) + off) << 8 | (key & 0xff);
+  }
+  return decode_key(best, first_bad);
+}
+
+int current_device() {
+  int d = 0;
+  if (hipGetDevice(&d) != hipSuccess) return -1;
+  return d;
+}
+
+int run_dev(CodecOp op, const void* d_in, size_t n, void* d_out, uint32_t flags, uint64_t* d_bad_key,
+            uint8_t* d_status, void* stream) {
+  if (!d_bad_key) return KZGPOT_E_INVALID_ARG;
+  if (n && (!d_in || !d_out)) return KZGPOT_E_INVALID_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  HIP_TRY(hipMemsetAsync(d_bad_key, 0xff, sizeof(uint64_t), s));
+  HIP_TRY(launch_codec(op, d_in, d_out, n, flags, (unsigned long long*)d_bad_key, d_status, s));
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int kzgpot_g1_decompress_ex(const uint8_t* in, size_t n, uint8_t* out, uint32_t flags, int64_t* first_bad,
+                            uint8_t* status) {
+  return run_host(current_device(), CodecOp::G1Decompress, in, n, out, flags, first_bad, status);
+}
+int kzgpot_g2_decompress_ex(const uint8_t* in, size_t n, uint8_t* out, uint32_t flags, int64_t* first_bad,
+                            uint8_t* status) {
+  return run_host(current_device(), CodecOp::G2Decompress, in, n, out, flags, first_bad, status);
+}
+int kzgpot_g1_transcode_uncompressed_ex(const uint8_t* in, size_t n, uint8_t* out, uint32_t flags,
+                                        int64_t* first_bad, uint8_t* status) {
+  return run_host(current_device(), CodecOp::G1Transcode, in, n, out, flags & KZGPOT_SUBGROUP_REF, first_bad,
+                  status);
+}
+int kzgpot_g2_transcode_uncompressed_ex(const uint8_t* in, size_t n, uint8_t* out, uint32_t flags,
+                                        int64_t* first_bad, uint8_t* status) {
+  return run_host(current_device(), CodecOp::G2Transcode, in, n, out, flags & KZGPOT_SUBGROUP_REF, first_bad,
+                  status);
+}
+int kzgpot_g1_decompress(const uint8_t* in, size_t n, uint8_t* out, uint32_t flags, int64_t* first_bad) {
+  return kzgpot_g1_decompress_ex(in, n, out, flags, first_bad, nullptr);
+}
+int kzgpot_g2_decompress(const uint8_t* in, size_t n, uint8_t* out, uint32_t flags, int64_t* first_bad) {
+  return kzgpot_g2_decompress_ex(in, n, out, flags, first_bad, nullptr);
+}
+int kzgpot_g1_transcode_uncompressed(const uint8_t* in, size_t n, uint8_t* out, uint32_t flags,
+                                     int64_t* first_bad) {
+  return kzgpot_g1_transcode_uncompressed_ex(in, n, out, flags, first_bad, nullptr);
+}
+int kzgpot_g2_transcode_uncompressed(const uint8_t* in, size_t n, uint8_t* out, uint32_t flags,
+                                     int64_t* first_bad) {
+  return kzgpot_g2_transcode_uncompressed_ex(in, n, out, flags, first_bad, nullptr);
+}
+
+int kzgpot_g1_decompress_dev(const void* d_in, size_t n, void* d_out, uint32_t flags, uint64_t* d_bad_key,
+                             uint8_t* d_status, void* stream) {
+  return run_dev(CodecOp::G1Decompress, d_in, n, d_out, flags, d_bad_key, d_status, stream);
+}
+int kzgpot_g2_decompress_dev(const void* d_in, size_t n, void* d_out, uint32_t flags, uint64_t* d_bad_key,
+                             uint8_t* d_status, void* stream) {
+  return run_dev(CodecOp::G2Decompress, d_in, n, d_out, flags, d_bad_key, d_status, stream);
+}
+int kzgpot_g1_transcode_uncompressed_dev(const void* d_in, size_t n, void* d_out, uint32_t flags,
+                                         uint64_t* d_bad_key, uint8_t* d_status, void* stream) {
+  return run_dev(CodecOp::G1Transcode, d_in, n, d_out, flags & KZGPOT_SUBGROUP_REF, d_bad_key, d_status, stream);
+}
+int kzgpot_g2_transcode_uncompressed_dev(const void* d_in, size_t n, void* d_out, uint32_t flags,
+                                         uint64_t* d_bad_key, uint8_t* d_status, void* stream) {
+  return run_dev(CodecOp::G2Transcode, d_in, n, d_out, flags & KZGPOT_SUBGROUP_REF, d_bad_key, d_status, stream);
+}
+int kzgpot_decode_bad_key(uint64_t key, int64_t* first_bad) { return decode_key(key, first_bad); }
+
+// ------------------------------------------------------------------------------- file pipeline
+uint64_t kzgpot_contribution_size(uint32_t n_log2) {
+  const uint64_t n = 1ull << n_log2;
+  return (2 * n - 1) * 48 + n * 96 + 2 * n * 48 + 96 + (3 * 192 + 6 * 96) + 64;
+}
+uint64_t kzgpot_output_size(uint32_t n_log2, int mode) {
+  const uint64_t n = 1ull << n_log2;
+  return mode == KZGPOT_MODE_FASTKZG ? (2 * n - 1) * 96 + n * 96 + 2 * 192 + n * 192
+                                     : (2 * n - 1) * 96 + n * 96 + 576;
+}
+
+int kzgpot_preprocess_buffer(const uint8_t* tr, size_t len, uint8_t* out, int mode, uint32_t n_log2, int n_gpus,
+                             int* bad_section, int64_t* bad_index) {
+  if (bad_section) *bad_section = -1;
+  if (bad_index) *bad_index = -1;
+  if (!tr || !out || n_log2 > 30 || (mode != KZGPOT_MODE_KZG && mode != KZGPOT_MODE_FASTKZG))
+    return KZGPOT_E_INVALID_ARG;
+  if (len != kzgpot_contribution_size(n_log2)) return KZGPOT_E_SIZE;
+  const int ndev = device_count();
+  if (ndev <= 0) return KZGPOT_E_DEVICE;
+  if (n_gpus <= 0 || n_gpus > ndev) n_gpus = ndev;
+  const uint64_t n = 1ull << n_log2;
+  // powersoftau Accumulator section order (after the 64-B hash)
+  const uint64_t cnt[5] = {2 * n - 1, n, n, n, 1};
+  const bool g2[5] = {false, true, false, false, true};
+  // read back by read_g1/read_g2 (checked) in each binary: kgz τG1, τG2, ατG1; fastkgz + βτG1
+  const bool checked[5] = {true, true, true, mode == KZGPOT_MODE_FASTKZG, false};
+  std::vector<std::vector<uint8_t>> sec(5);
+  int ret = 0;
+  const uint8_t* p = tr + 64;
+  for (int s = 0; s < 5; s++) {
+    const CodecOp op = g2[s] ? CodecOp::G2Decompress : CodecOp::G1Decompress;
+    const uint64_t rin = in_record(op), rout = out_record(op);
+    sec[s].resize(cnt[s] * rout);
+    const uint32_t fl = checked[s] ? 0u : KZGPOT_NO_SUBGROUP_CHECK;
+    // contiguous shards, one host thread per GPU
+    std::vector<int> rc(n_gpus, 0);
+    std::vector<int64_t> fb(n_gpus, -1);
+    std::vector<std::thread> th;
+    const uint64_t per = (cnt[s] + n_gpus - 1) / n_gpus;
+    for (int g = 0; g < n_gpus; g++) {
+      const uint64_t lo = std::min(cnt[s], g * per), hi = std::min(cnt[s], lo + per);
+      th.emplace_back([&, g, lo, hi] {
+        rc[g] = run_host(g, op, p + lo * rin, hi - lo, sec[s].data() + lo * rout, fl, &fb[g], nullptr);
+        if (fb[g] >= 0) fb[g] += (int64_t)lo;
+      });
+    }
+    for (auto& t : th) t.join();
+    for (int g = 0; g < n_gpus && !ret; g++)
+      if (rc[g]) {
+        ret = rc[g];
+        if (bad_section) *bad_section = s;
+        if (bad_index) *bad_index = fb[g];
+      }
+    p += cnt[s] * rin;
+  }
+  if (ret) return ret;
+  uint8_t* o = out;
+  auto put = [&](const uint8_t* src, size_t bytes) {
+    memcpy(o, src, bytes);
+    o += bytes;
+  };
+  put(sec[0].data(), sec[0].size());  // powers_of_g = τG1
+  put(sec[2].data(), sec[2].size());  // powers_of_gamma_g = ατG1 (BTreeMap key order in fastkgz)
+  if (mode == KZGPOT_MODE_KZG) {      // VerifierKey{g, gamma_g, h, beta_h} (preprocess-kgz.rs:177-194)
+    put(sec[0].data(), 96);
+    put(sec[2].data(), 96);
+    put(sec[1].data(), 192);
+    put(sec[1].data() + 192, 192);
+  } else {                            // h, beta_h, neg_powers_of_h (empty), powers_of_h (fkgz:200-208)
+    put(sec[1].data(), 192);
+    put(sec[1].data() + 192, 192);
+    put(sec[1].data(), sec[1].size());
+  }
+  return 0;
+}
+
+int kzgpot_preprocess(const char* transcript_path, const char* out_path, int mode, uint32_t n_log2, int n_gpus,
+                      int* bad_section, int64_t* bad_index) {
+  if (!transcript_path || !out_path) return KZGPOT_E_INVALID_ARG;
+  FILE* f = fopen(transcript_path, "rb");
+  if (!f) return KZGPOT_E_IO;
+  fseek(f, 0, SEEK_END);
+  const long len = ftell(f);
+  fseek(f, 0, SEEK_SET);
+  if (len < 0 || (uint64_t)len != kzgpot_contribution_size(n_log2)) {
+    fclose(f);
+    return KZGPOT_E_SIZE;
+  }
+  std::vector<uint8_t> tr((size_t)len);
+  const size_t got = fread(tr.data(), 1, tr.size(), f);
+  fclose(f);
+  if (got != tr.size()) return KZGPOT_E_IO;
+  std::vector<uint8_t> out(kzgpot_output_size(n_log2, mode));
+  const int r = kzgpot_preprocess_buffer(tr.data(), tr.size(), out.data(), mode, n_log2, n_gpus, bad_section,
+                                         bad_index);
+  if (r) return r;
+  FILE* o = fopen(out_path, "wb");
+  if (!o) return KZGPOT_E_IO;
+  const size_t put = fwrite(out.data(), 1, out.size(), o);
+  const int cr = fclose(o);
+  return (put == out.size() && cr == 0) ? 0 : KZGPOT_E_IO;
+}
+
+const char* kzgpot_status_name(int s) {
+  switch (s < 0 && s > -100 ? -s : s) {
+    case KZGPOT_OK: return "ok";
+    case KZGPOT_ST_COMPRESSION_MODE: return "UnexpectedCompressionMode";
+    case KZGPOT_ST_UNEXPECTED_INFO: return "UnexpectedInformation";
+    case KZGPOT_ST_NOT_IN_FIELD: return "NotInField";
+    case KZGPOT_ST_NOT_ON_CURVE: return "NotOnCurve";
+    case KZGPOT_ST_NOT_IN_SUBGROUP: return "NotInSubgroup";
+    case KZGPOT_ST_UNEXPECTED_FLAGS: return "UnexpectedFlags";
+    case KZGPOT_ST_INFINITY: return "Infinity";
+    case KZGPOT_E_INVALID_ARG: return "InvalidArgument";
+    case KZGPOT_E_DEVICE: return "DeviceError";
+    case KZGPOT_E_IO: return "IoError";
+    case KZGPOT_E_SIZE: return "SizeMismatch";
+    case KZGPOT_E_DIGEST: return "DigestMismatch";
+    case KZGPOT_E_NETWORK: return "NetworkUnavailable";
+    default: return "unknown";
+  }
+}
+int kzgpot_device_count(void) { return device_count(); }
+const char* kzgpot_version(void) { return "kzgpot 0.1.0 (gfx950)"; }
+
+}  // extern "C"

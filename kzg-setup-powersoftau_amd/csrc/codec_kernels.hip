@@ -1,0 +1,447 @@
+// The hot path: one lane per point, decompress -> check -> arkworks emit, in two kernel phases.
+//
+// Replaces, per point, the reference's three CPU passes:
+//   powersoftau Accumulator::deserialize → pairing into_affine_unchecked   (preprocess-kgz.rs:105)
+//   Accumulator::serialize(UseCompression::No) → 1.2 GB intermediate file   (preprocess-kgz.rs:122)
+//   read_g1 / read_g2 → ark deserialize_uncompressed (subgroup check)     (src/lib.rs:41-80)
+//   serialize_uncompressed into the kzg_setup file                       (preprocess-kgz.rs:188-194)
+// The intermediate never exists: for a finite point the ark bytes are the per-coordinate byte
+// reversal of the pairing bytes (G2 also swaps c0/c1), so phase 1 emits them directly and phase 2
+// checks them in place.
+//
+//   phase 1  k_gX_decompress : flags, x < p, Fp/Fp2 square root, sign rule → ark record
+//                              (rejected points get a poison record: x's top limb = 0xffffffff)
+//   phase 2  k_gX_check<Src> : ark deserialize_uncompressed on the record — x, y < p, SWFlags,
+//                              subgroup — in place on phase 1's output (Src = ArkInPlace), or on a
+//                              pairing-uncompressed input for the read_g1/read_g2 transcode
+//                              (Src = PairingBE). Rejected records are zero-filled.
+// Splitting the phases keeps each kernel's live register set to one algorithm (the square-root
+// table or the scalar-multiplication state, not both), which is what sets occupancy here; the
+// extra traffic is one 96/192-B re-read per point, against ~1,500 Fp multiplies of work.
+//
+// HBM layout: packed records, no padding — G1 in 48 B (3 x 16-B loads per lane), out 96 B
+// (6 x 16-B stores); G2 in 96 B / out 192 B. All records are 16-B aligned.
+//
+// Status per point (first_bad = min index with a nonzero status, deterministic — the reference
+// keeps an arbitrary one under a Mutex and then panics):
+//   1 UnexpectedCompressionMode  2 UnexpectedInformation  3 NotInField  4 NotOnCurve
+//   5 NotInSubgroup  6 UnexpectedFlags  7 Infinity (reference panics: read_g1 sees x >= p)
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "codec.hpp"
+#include "curve.hpp"
+
+namespace kzgpot {
+
+constexpr uint32_t kPoison = 0xffffffffu;
+
+KZG_DEV uint32_t bswap32(uint32_t v) { return __builtin_bswap32(v); }
+
+KZG_DEV void report(uint64_t i, int st, unsigned long long* first_bad, uint8_t* status) {
+  if (status) status[i] = (uint8_t)st;
+  if (st) atomicMin(first_bad, (unsigned long long)((i << 8) | (uint64_t)st));
+}
+
+// Hide a pointer from the optimiser so loads through it are re-issued at every use (keeps the
+// affine base point out of the register file during the scalar-multiplication loops).
+template <typename T>
+KZG_DEV const T* opaque(const T* p) {
+  asm volatile("" : "+v"(p));
+  return p;
+}
+
+// canonical p - c (c canonical), with p - 0 mapped to 0
+KZG_DEV void neg_canon(fp& r, const fp& c) {
+  uint32_t br = 0;
+  const bool z = fp_is_zero_canon(c);
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    const uint32_t d = __builtin_subc(FP_P[i], c.v[i], br, &br);
+    r.v[i] = z ? 0u : d;
+  }
+}
+
+KZG_DEV void store2(uint4* dst, const fp& a, const fp& b) {  // 96 B: a LE then b LE
+  dst[0] = make_uint4(a.v[0], a.v[1], a.v[2], a.v[3]);
+  dst[1] = make_uint4(a.v[4], a.v[5], a.v[6], a.v[7]);
+  dst[2] = make_uint4(a.v[8], a.v[9], a.v[10], a.v[11]);
+  dst[3] = make_uint4(b.v[0], b.v[1], b.v[2], b.v[3]);
+  dst[4] = make_uint4(b.v[4], b.v[5], b.v[6], b.v[7]);
+  dst[5] = make_uint4(b.v[8], b.v[9], b.v[10], b.v[11]);
+}
+KZG_DEV void store_zero(uint4* dst, int n16) {
+#pragma unroll 1
+  for (int k = 0; k < n16; k++) dst[k] = make_uint4(0, 0, 0, 0);
+}
+KZG_DEV void load_le(fp& r, const uint4* src) {  // 48 little-endian bytes
+  const uint4 a = src[0], b = src[1], c = src[2];
+  r.v[0] = a.x, r.v[1] = a.y, r.v[2] = a.z, r.v[3] = a.w;
+  r.v[4] = b.x, r.v[5] = b.y, r.v[6] = b.z, r.v[7] = b.w;
+  r.v[8] = c.x, r.v[9] = c.y, r.v[10] = c.z, r.v[11] = c.w;
+}
+KZG_DEV void load_be(fp& r, const uint4* src) {  // 48 big-endian bytes
+  const uint4 a = src[0], b = src[1], c = src[2];
+  const uint32_t w[12] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w};
+#pragma unroll
+  for (int k = 0; k < 12; k++) r.v[k] = bswap32(w[11 - k]);
+}
+
+// ================================================================================ phase 1: G1
+__global__ void __launch_bounds__(kBlock) k_g1_decompress(const uint4* __restrict__ in, uint4* __restrict__ out,
+                                                          uint64_t n, uint32_t flags,
+                                                          unsigned long long* __restrict__ first_bad,
+                                                          uint8_t* __restrict__ status) {
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const bool checked = !(flags & KZGPOT_NO_SUBGROUP_CHECK);
+  fp x;
+  load_be(x, in + i * 3);
+  const uint32_t b0 = x.v[11] >> 24;  // first byte on the wire
+  uint32_t rest = 0;
+#pragma unroll
+  for (int k = 0; k < 11; k++) rest |= x.v[k];
+  const bool inf_clean = ((x.v[11] & 0x3fffffffu) | rest) == 0;  // copy[0] &= 0x3f; all zero?
+  x.v[11] &= 0x1fffffffu;
+
+  int st = 0;
+  if (!(b0 & 0x80u)) st = 1;
+  else if (b0 & 0x40u) st = inf_clean ? (checked ? 7 : 0) : 2;
+  else if (limbs_geq_p(x.v)) st = 3;
+  const bool is_inf = (b0 & 0xc0u) == 0xc0u && st == 0;
+  const bool greatest = (b0 & 0x20u) != 0;
+
+  // y = (x^3 + 4)^((p+1)/4); every lane runs the same chain (wave-uniform)
+  fp a, y, t;
+  fp_to_mont(t, x);
+  fp_sqr(a, t);
+  fp_mul(a, a, t);
+  fp_set(t, FP_FOUR);
+  fp_add(a, a, t);
+  fp_pow_pm3d4(t, a);
+  fp_mul(y, t, a);
+  fp_sqr(t, y);
+  if (st == 0 && !is_inf && !fp_eq(t, a)) st = 4;
+
+  // sign rule (pairing get_point_from_x): keep y if (y < -y) XOR greatest, canonical order
+  fp yc, nyc;
+  fp_from_mont(yc, y);
+  neg_canon(nyc, yc);
+  const bool keep = fp_lt_canon(yc, nyc) ^ greatest;
+
+  uint4* dst = out + i * 6;
+  if (st == 0 && !is_inf) {
+    fp_select(yc, keep, yc, nyc);
+    store2(dst, x, yc);
+  } else {
+    fp zx, zy;
+    fp_zero(zx);
+    fp_zero(zy);
+    if (is_inf) zy.v[0] = 1, zy.v[11] = 0x40000000u;  // ark GroupAffine::zero() = (0, 1, inf)
+    if (st && checked) zx.v[11] = kPoison;             // phase 2 zero-fills and skips it
+    store2(dst, zx, zy);
+  }
+  report(i, st, first_bad, status);
+}
+
+// ================================================================================ phase 1: G2
+// Fp2 square root without Algorithm 9's data-dependent branches (any root works: the sign
+// rule normalises it). With N = a0^2 + a1^2 (a is a square in Fp2 iff N is one in Fp):
+//   gam = sqrt(N); d = (a0 + gam)/2 (d = a0 if that is 0); t = d^((p-3)/4); s = t d
+//   s^2 == d  ->  y = (s, a1 t / 2)      else (s^2 = -d, t s = -1)  ->  y = (-a1 t / 2, s)
+// and y is accepted iff gam^2 == N and y^2 == a. Two Fp exponentiations (~920 Fp multiplies)
+// where Algorithm 9 needs two Fp2 ones (~2,700).
+KZG_DEV bool fp2_sqrt(fp2& y, const fp2& a) {
+  fp nrm, t0, gam, d, s, h, inv2;
+  fp_sqr(nrm, a.c0);
+  fp_sqr(t0, a.c1);
+  fp_add(nrm, nrm, t0);
+  fp_pow_pm3d4(t0, nrm);
+  fp_mul(gam, t0, nrm);
+  fp_sqr(t0, gam);
+  const bool ok1 = fp_eq(t0, nrm);
+  fp_set(inv2, FP_INV2);
+  fp_add(d, a.c0, gam);
+  fp_mul(d, d, inv2);
+  fp_select(d, fp_is_zero(d), a.c0, d);
+  fp_pow_pm3d4(t0, d);  // t
+  fp_mul(s, t0, d);
+  fp_mul(h, a.c1, t0);
+  fp_mul(h, h, inv2);
+  fp_sqr(t0, s);
+  const bool case1 = fp_eq(t0, d);
+  fp nh;
+  fp_neg(nh, h);
+  fp_select(y.c0, case1, s, nh);
+  fp_select(y.c1, case1, h, s);
+  fp2 y2;
+  f_sqr(y2, y);
+  f_sub(y2, y2, a);
+  return ok1 && f_is_zero(y2);
+}
+
+__global__ void __launch_bounds__(kBlock) k_g2_decompress(const uint4* __restrict__ in, uint4* __restrict__ out,
+                                                          uint64_t n, uint32_t flags,
+                                                          unsigned long long* __restrict__ first_bad,
+                                                          uint8_t* __restrict__ status) {
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const bool checked = !(flags & KZGPOT_NO_SUBGROUP_CHECK);
+  fp2 x;  // wire order: x.c1 ‖ x.c0
+  load_be(x.c1, in + i * 6);
+  load_be(x.c0, in + i * 6 + 3);
+  const uint32_t b0 = x.c1.v[11] >> 24;
+  uint32_t rest = x.c0.v[11];
+#pragma unroll
+  for (int k = 0; k < 11; k++) rest |= x.c1.v[k] | x.c0.v[k];
+  const bool inf_clean = ((x.c1.v[11] & 0x3fffffffu) | rest) == 0;
+  x.c1.v[11] &= 0x1fffffffu;
+
+  int st = 0;
+  if (!(b0 & 0x80u)) st = 1;
+  else if (b0 & 0x40u) st = inf_clean ? (checked ? 7 : 0) : 2;
+  else if (limbs_geq_p(x.c0.v) || limbs_geq_p(x.c1.v)) st = 3;
+  const bool is_inf = (b0 & 0xc0u) == 0xc0u && st == 0;
+  const bool greatest = (b0 & 0x20u) != 0;
+
+  fp2 a, y, t;
+  fp_to_mont(t.c0, x.c0);
+  fp_to_mont(t.c1, x.c1);
+  f_sqr(a, t);
+  f_mul(a, a, t);
+  fp_set(t.c0, FP_FOUR);
+  t.c1 = t.c0;
+  f_add(a, a, t);  // x^3 + 4(1 + u)
+  const bool on = fp2_sqrt(y, a);
+  if (st == 0 && !is_inf && !on) st = 4;
+
+  // pairing Ord for Fq2: lexicographic, c1 first
+  fp2 yc, nyc;
+  fp_from_mont(yc.c0, y.c0);
+  fp_from_mont(yc.c1, y.c1);
+  neg_canon(nyc.c0, yc.c0);
+  neg_canon(nyc.c1, yc.c1);
+  bool c1eq = true;
+#pragma unroll
+  for (int k = 0; k < 12; k++) c1eq = c1eq && (yc.c1.v[k] == nyc.c1.v[k]);
+  const bool lt = c1eq ? fp_lt_canon(yc.c0, nyc.c0) : fp_lt_canon(yc.c1, nyc.c1);
+  const bool keep = lt ^ greatest;
+
+  uint4* dst = out + i * 12;
+  if (st == 0 && !is_inf) {
+    fp_select(yc.c0, keep, yc.c0, nyc.c0);
+    fp_select(yc.c1, keep, yc.c1, nyc.c1);
+    store2(dst, x.c0, x.c1);
+    store2(dst + 6, yc.c0, yc.c1);
+  } else {
+    fp z, zy0, zy1;
+    fp_zero(z);
+    fp_zero(zy0);
+    fp_zero(zy1);
+    if (is_inf) zy0.v[0] = 1, zy1.v[11] = 0x40000000u;  // ark zero() = ((0,0), (1,0), inf)
+    fp zx = z;
+    if (st && checked) zx.v[11] = kPoison;
+    store2(dst, zx, z);
+    store2(dst + 6, zy0, zy1);
+  }
+  report(i, st, first_bad, status);
+}
+
+// ================================================================================ phase 2
+// ark-ec 0.2 deserialize_uncompressed on one record, then serialize_uncompressed.
+//   Src::ArkInPlace : the record is phase 1's output (ark LE, x ‖ y)           — decompress path
+//   Src::PairingBE  : pairing-uncompressed input; read_g1 (src/lib.rs:41-54) / read_g2
+//                     (src/lib.rs:56-80) byte order is applied on load        — transcode path
+// The reference checks no curve equation: points on the curve take the endomorphism test, the
+// rest the exact ark double-and-add by r (divergent, but only for inputs that are not points).
+enum class Src { ArkInPlace, PairingBE };
+
+template <Src S>
+struct G1Rec {
+  // field offsets in 16-B units inside one record
+  static KZG_DEV void load_xy(fp& x, fp& y, const uint4* rec) {
+    if constexpr (S == Src::ArkInPlace) {
+      load_le(x, rec);
+      load_le(y, rec + 3);
+    } else {
+      load_be(x, rec);
+      load_be(y, rec + 3);
+    }
+  }
+};
+
+template <Src S>
+__global__ void __launch_bounds__(kBlock) k_g1_check(const uint4* __restrict__ in, uint4* __restrict__ out,
+                                                     uint64_t n, uint32_t flags,
+                                                     unsigned long long* __restrict__ first_bad,
+                                                     uint8_t* __restrict__ status) {
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const uint4* rec = (S == Src::ArkInPlace ? (const uint4*)out : in) + i * 6;
+  uint4* dst = out + i * 6;
+  fp x, y;
+  G1Rec<S>::load_xy(x, y, rec);
+  if (S == Src::ArkInPlace && x.v[11] == kPoison) {  // phase 1 already rejected (and reported) it
+    store_zero(dst, 6);
+    return;
+  }
+  const uint32_t yb = y.v[11] >> 24;  // ark SWFlags: top byte of y
+  const bool fpos = yb & 0x80u, finf = yb & 0x40u;
+  y.v[11] &= 0x3fffffffu;
+  int st = 0;
+  if (limbs_geq_p(x.v)) st = 3;
+  else if (fpos && finf) st = 6;
+  else if (limbs_geq_p(y.v)) st = 3;
+
+  if (st == 0 && !finf) {
+    auto load = [&](fp& bx, fp& by) {
+      fp cx, cy;
+      G1Rec<S>::load_xy(cx, cy, opaque(rec));
+      cy.v[11] &= 0x3fffffffu;
+      fp_to_mont(bx, cx);
+      fp_to_mont(by, cy);
+    };
+    bool on_curve;
+    {
+      fp xm, ym, l, r;
+      load(xm, ym);
+      fp_sqr(l, ym);
+      fp_sqr(r, xm);
+      fp_mul(r, r, xm);
+      fp_set(xm, FP_FOUR);
+      fp_add(r, r, xm);
+      on_curve = fp_eq(l, r);
+    }
+    bool ok;
+    if ((flags & KZGPOT_SUBGROUP_REF) || !on_curve)
+      ok = in_subgroup_ref<fp>(load);
+    else
+      ok = in_subgroup_fast_g1(load);
+    if (!ok) st = 5;
+  }
+  if (st) {
+    store_zero(dst, 6);
+  } else if (S == Src::PairingBE) {
+    if (finf) y.v[11] |= 0x40000000u;  // GroupAffine::new(x, y, true) keeps x, y
+    store2(dst, x, y);
+  }
+  report(i, st, first_bad, status);
+}
+
+template <Src S>
+struct G2Rec {
+  static KZG_DEV void load_xy(fp2& x, fp2& y, const uint4* rec) {
+    if constexpr (S == Src::ArkInPlace) {  // x.c0, x.c1, y.c0, y.c1 (LE)
+      load_le(x.c0, rec);
+      load_le(x.c1, rec + 3);
+      load_le(y.c0, rec + 6);
+      load_le(y.c1, rec + 9);
+    } else {  // wire: x.c1, x.c0, y.c1, y.c0 (BE)
+      load_be(x.c1, rec);
+      load_be(x.c0, rec + 3);
+      load_be(y.c1, rec + 6);
+      load_be(y.c0, rec + 9);
+    }
+  }
+};
+
+template <Src S>
+__global__ void __launch_bounds__(kBlock) k_g2_check(const uint4* __restrict__ in, uint4* __restrict__ out,
+                                                     uint64_t n, uint32_t flags,
+                                                     unsigned long long* __restrict__ first_bad,
+                                                     uint8_t* __restrict__ status) {
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const uint4* rec = (S == Src::ArkInPlace ? (const uint4*)out : in) + i * 12;
+  uint4* dst = out + i * 12;
+  fp2 x, y;
+  G2Rec<S>::load_xy(x, y, rec);
+  if (S == Src::ArkInPlace && x.c0.v[11] == kPoison) {
+    store_zero(dst, 12);
+    return;
+  }
+  const uint32_t yb = y.c1.v[11] >> 24;
+  const bool fpos = yb & 0x80u, finf = yb & 0x40u;
+  y.c1.v[11] &= 0x3fffffffu;
+  int st = 0;
+  if (limbs_geq_p(x.c0.v) || limbs_geq_p(x.c1.v)) st = 3;
+  else if (limbs_geq_p(y.c0.v)) st = 3;
+  else if (fpos && finf) st = 6;
+  else if (limbs_geq_p(y.c1.v)) st = 3;
+
+  if (st == 0 && !finf) {
+    auto load = [&](fp2& bx, fp2& by) {
+      fp2 cx, cy;
+      G2Rec<S>::load_xy(cx, cy, opaque(rec));
+      cy.c1.v[11] &= 0x3fffffffu;
+      fp_to_mont(bx.c0, cx.c0);
+      fp_to_mont(bx.c1, cx.c1);
+      fp_to_mont(by.c0, cy.c0);
+      fp_to_mont(by.c1, cy.c1);
+    };
+    bool on_curve;
+    {
+      fp2 xm, ym, l, r;
+      load(xm, ym);
+      f_sqr(l, ym);
+      f_sqr(r, xm);
+      f_mul(r, r, xm);
+      fp_set(xm.c0, FP_FOUR);
+      xm.c1 = xm.c0;
+      f_add(r, r, xm);
+      f_sub(l, l, r);
+      on_curve = f_is_zero(l);
+    }
+    bool ok;
+    if ((flags & KZGPOT_SUBGROUP_REF) || !on_curve)
+      ok = in_subgroup_ref<fp2>(load);
+    else
+      ok = in_subgroup_fast_g2(load);
+    if (!ok) st = 5;
+  }
+  if (st) {
+    store_zero(dst, 12);
+  } else if (S == Src::PairingBE) {
+    if (finf) y.c1.v[11] |= 0x40000000u;
+    store2(dst, x.c0, x.c1);
+    store2(dst + 6, y.c0, y.c1);
+  }
+  report(i, st, first_bad, status);
+}
+
+// ================================================================================ launchers
+static inline unsigned grid_for(uint64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
+
+hipError_t launch_codec(CodecOp op, const void* d_in, void* d_out, uint64_t n, uint32_t flags,
+                        unsigned long long* d_first_bad, uint8_t* d_status, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  const dim3 grid(grid_for(n)), block(kBlock);
+  const uint4* in = (const uint4*)d_in;
+  uint4* out = (uint4*)d_out;
+  const bool checked = !(flags & KZGPOT_NO_SUBGROUP_CHECK);
+  switch (op) {
+    case CodecOp::G1Decompress:
+      hipLaunchKernelGGL(k_g1_decompress, grid, block, 0, stream, in, out, n, flags, d_first_bad, d_status);
+      if (checked)
+        hipLaunchKernelGGL(k_g1_check<Src::ArkInPlace>, grid, block, 0, stream, in, out, n, flags, d_first_bad,
+                           d_status);
+      break;
+    case CodecOp::G2Decompress:
+      hipLaunchKernelGGL(k_g2_decompress, grid, block, 0, stream, in, out, n, flags, d_first_bad, d_status);
+      if (checked)
+        hipLaunchKernelGGL(k_g2_check<Src::ArkInPlace>, grid, block, 0, stream, in, out, n, flags, d_first_bad,
+                           d_status);
+      break;
+    case CodecOp::G1Transcode:
+      hipLaunchKernelGGL(k_g1_check<Src::PairingBE>, grid, block, 0, stream, in, out, n, flags, d_first_bad,
+                         d_status);
+      break;
+    case CodecOp::G2Transcode:
+      hipLaunchKernelGGL(k_g2_check<Src::PairingBE>, grid, block, 0, stream, in, out, n, flags, d_first_bad,
+                         d_status);
+      break;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace kzgpot

@@ -1,0 +1,206 @@
+"""kzgpot — MI355X-native Powers-of-Tau → arkworks KZG preprocessor (Python host side).
+
+Mirrors the reference crate's surface (heliaxdev/kzg-setup-powersoftau, `src/lib.rs`) above the
+C ABI in `include/kzgpot.h`:
+
+  read_g1 / read_g2            src/lib.rs:41-80     (batched: whole record streams per call)
+  load_kzg_setup               src/lib.rs:174-195
+  load_fastkzg_setup           src/lib.rs:197-228
+  download_kzg_setup /
+  download_fastkzg_setup       src/lib.rs:166-172   (no network in this build: local file + digest)
+  preprocess_kgz /
+  preprocess_fastkgz           src/bin/preprocess-{kgz,fastkgz}.rs main
+
+Every compute call runs the HIP kernels; errors raise `KzgPotError` (the reference `unwrap()`s
+and panics on the first bad point — preprocess-kgz.rs:110,142).
+"""
+from __future__ import annotations
+
+import ctypes
+import hashlib
+import os
+from dataclasses import dataclass
+
+from . import _lib
+
+KZG_SETUP_FILE = "kzg_setup"                               # src/lib.rs:20
+KZG_SETUP_FILE_DIGEST = (                                  # src/lib.rs:21
+    "87932f626204ab9a5d4be67ef2ee479471baf942364ada2f89840a2afec8925911fb88cb77024e66d759b4970b25cf2a7b03d1fc8c15768e021220b8ba21efcf")
+FASTKZG_SETUP_FILE_DIGEST = (                              # src/lib.rs:22
+    "d177841ad145c0d526e56a8d2cde473f09e85944f5c5d6b72d8063e4a199f8a6fca0b0f6ee91ef79df48518b5edd8165bbdecf0fe4eb0d29809032878f8b17ce")
+POWERSOFTAU_DIGEST = (                                     # src/bin/preprocess-kgz.rs:19
+    "88dc1dc6914e44568e8511eace177e6ecd9da9a9bd8f67e4c0c9f215b517db4d1d54a755d051978dbb85ef947918193c93cd4cf4c99c0dc5a767d4eeb10047a4")
+TAU_POWERS_LOG2 = 21                                       # src/lib.rs:23
+TAU_POWERS_LENGTH = 1 << TAU_POWERS_LOG2
+TAU_POWERS_G1_LENGTH = (TAU_POWERS_LENGTH << 1) - 1        # src/lib.rs:24
+
+NO_SUBGROUP_CHECK = 0x1
+SUBGROUP_REF = 0x2
+MODE_KZG = 0
+MODE_FASTKZG = 1
+
+ST_OK, ST_COMPRESSION_MODE, ST_UNEXPECTED_INFO, ST_NOT_IN_FIELD = 0, 1, 2, 3
+ST_NOT_ON_CURVE, ST_NOT_IN_SUBGROUP, ST_UNEXPECTED_FLAGS, ST_INFINITY = 4, 5, 6, 7
+SECTIONS = ("tau_g1", "tau_g2", "alpha_g1", "beta_g1", "beta_g2")
+
+
+class KzgPotError(RuntimeError):
+    def __init__(self, code: int, first_bad: int = -1, section: int = -1):
+        self.code = code
+        self.first_bad = first_bad
+        self.section = section
+        name = status_name(code)
+        where = f" at index {first_bad}" if first_bad >= 0 else ""
+        if section >= 0:
+            where += f" in section {SECTIONS[section]}"
+        super().__init__(f"kzgpot error {code} ({name}){where}")
+
+
+def status_name(code: int) -> str:
+    return _lib.load().kzgpot_status_name(code).decode()
+
+
+def device_count() -> int:
+    return _lib.load().kzgpot_device_count()
+
+
+def version() -> str:
+    return _lib.load().kzgpot_version().decode()
+
+
+@dataclass
+class CodecResult:
+    out: bytes
+    ret: int
+    first_bad: int
+    status: bytes | None
+
+
+def _buf(data) -> tuple[ctypes.c_void_p, int, object]:
+    if isinstance(data, (bytes, bytearray, memoryview)):
+        b = bytes(data)
+        return ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p), len(b), b
+    import numpy as np  # numpy arrays (uint8, C-contiguous)
+    arr = np.ascontiguousarray(data, dtype=np.uint8)
+    return ctypes.c_void_p(arr.ctypes.data), arr.nbytes, arr
+
+
+_OPS = {
+    "g1_decompress": ("kzgpot_g1_decompress_ex", 48, 96),
+    "g2_decompress": ("kzgpot_g2_decompress_ex", 96, 192),
+    "g1_transcode": ("kzgpot_g1_transcode_uncompressed_ex", 96, 96),
+    "g2_transcode": ("kzgpot_g2_transcode_uncompressed_ex", 192, 192),
+}
+
+
+def run_codec(op: str, data, flags: int = 0, want_status: bool = False) -> CodecResult:
+    """Run one batched codec op over a packed record stream on the current GPU."""
+    fname, rin, rout = _OPS[op]
+    ptr, nbytes, keep = _buf(data)
+    if nbytes % rin:
+        raise ValueError(f"{op}: input length {nbytes} is not a multiple of {rin}")
+    n = nbytes // rin
+    out = ctypes.create_string_buffer(max(1, n * rout))
+    st = ctypes.create_string_buffer(max(1, n)) if want_status else None
+    fb = ctypes.c_int64(-1)
+    ret = getattr(_lib.load(), fname)(ptr, n, out, flags, ctypes.byref(fb), st)
+    del keep
+    if ret <= -100:
+        raise KzgPotError(ret)
+    return CodecResult(out.raw[: n * rout], ret, fb.value, st.raw[:n] if st is not None else None)
+
+
+def g1_decompress(data, flags: int = 0, want_status: bool = False) -> CodecResult:
+    return run_codec("g1_decompress", data, flags, want_status)
+
+
+def g2_decompress(data, flags: int = 0, want_status: bool = False) -> CodecResult:
+    return run_codec("g2_decompress", data, flags, want_status)
+
+
+def _checked(res: CodecResult) -> bytes:
+    if res.ret != 0:
+        raise KzgPotError(res.ret, res.first_bad)
+    return res.out
+
+
+def read_g1(reader, count: int = 1, flags: int = 0) -> bytes:
+    """src/lib.rs:41-54 read_g1, batched: reads `count` 96-B pairing-uncompressed G1 records from
+    `reader` and returns their ark `serialize_uncompressed` bytes (subgroup-checked). Raises on the
+    first invalid point, as the reference's callers `unwrap()`."""
+    data = reader.read(96 * count)
+    if len(data) != 96 * count:
+        raise EOFError("read_g1: short read")  # reference: read_exact(..).unwrap()
+    return _checked(run_codec("g1_transcode", data, flags))
+
+
+def read_g2(reader, count: int = 1, flags: int = 0) -> bytes:
+    """src/lib.rs:56-80 read_g2, batched (192-B records, x.c1‖x.c0‖y.c1‖y.c0 → ark c0,c1 order)."""
+    data = reader.read(192 * count)
+    if len(data) != 192 * count:
+        raise EOFError("read_g2: short read")
+    return _checked(run_codec("g2_transcode", data, flags))
+
+
+def contribution_size(n_log2: int = TAU_POWERS_LOG2) -> int:
+    return _lib.load().kzgpot_contribution_size(n_log2)
+
+
+def output_size(n_log2: int = TAU_POWERS_LOG2, mode: int = MODE_KZG) -> int:
+    return _lib.load().kzgpot_output_size(n_log2, mode)
+
+
+def preprocess_buffer(transcript, n_log2: int, mode: int = MODE_KZG, n_gpus: int = 0) -> bytes:
+    """preprocess-{kgz,fastkgz} main on an in-memory response transcript → output file bytes."""
+    ptr, nbytes, keep = _buf(transcript)
+    out = ctypes.create_string_buffer(output_size(n_log2, mode))
+    sec, idx = ctypes.c_int(-1), ctypes.c_int64(-1)
+    r = _lib.load().kzgpot_preprocess_buffer(ptr, nbytes, out, mode, n_log2, n_gpus, ctypes.byref(sec),
+                                             ctypes.byref(idx))
+    del keep
+    if r:
+        raise KzgPotError(r, idx.value, sec.value)
+    return out.raw
+
+
+def preprocess(transcript_path: str, out_path: str = KZG_SETUP_FILE, mode: int = MODE_KZG,
+               n_log2: int = TAU_POWERS_LOG2, n_gpus: int = 0) -> None:
+    """`preprocess-kgz` / `preprocess-fastkgz` without the download step (no network here)."""
+    sec, idx = ctypes.c_int(-1), ctypes.c_int64(-1)
+    r = _lib.load().kzgpot_preprocess(transcript_path.encode(), out_path.encode(), mode, n_log2, n_gpus,
+                                      ctypes.byref(sec), ctypes.byref(idx))
+    if r:
+        raise KzgPotError(r, idx.value, sec.value)
+
+
+def preprocess_kgz(transcript_path: str = "powersoftau", out_path: str = KZG_SETUP_FILE, **kw) -> None:
+    preprocess(transcript_path, out_path, MODE_KZG, **kw)
+
+
+def preprocess_fastkgz(transcript_path: str = "powersoftau", out_path: str = KZG_SETUP_FILE, **kw) -> None:
+    preprocess(transcript_path, out_path, MODE_FASTKZG, **kw)
+
+
+def blake2b_hex(data: bytes) -> str:
+    """blake2b_simd::State::new().update(data).finalize().to_hex() (src/lib.rs:129)."""
+    return hashlib.blake2b(data).hexdigest()
+
+
+def _download_setup(file_digest: str, check_digest: bool, path: str = KZG_SETUP_FILE) -> None:
+    """src/lib.rs:123-164 without the HTTPS fetch (no network in this build). A local file is
+    accepted as the reference does; with check_digest a mismatch RAISES (the reference silently
+    returns Ok on mismatch, lib.rs:133-143 — a bug not reproduced)."""
+    if not os.path.exists(path):
+        raise KzgPotError(-105)
+    if check_digest:
+        with open(path, "rb") as f:
+            if blake2b_hex(f.read()) != file_digest:
+                raise KzgPotError(-104)
+
+
+def download_kzg_setup(check_digest: bool, path: str = KZG_SETUP_FILE) -> None:
+    _download_setup(KZG_SETUP_FILE_DIGEST, check_digest, path)
+
+
+def download_fastkzg_setup(check_digest: bool, path: str = KZG_SETUP_FILE) -> None:
+    _download_setup(FASTKZG_SETUP_FILE_DIGEST, check_digest, path)
