@@ -1,0 +1,88 @@
+"""N > 1 path on CPU: world_size-2 gloo processes shard a G1 stream, decode their shards (with the
+C oracle standing in for the GPU kernels), reduce the first-bad key and all-gather one contiguous
+arkworks buffer — the same kzgpot.dist code bench.py runs over RCCL."""
+import ctypes
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import ROOT, golden
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, data, n, bad_index, q):
+    import sys
+
+    sys.path.insert(0, os.path.join(ROOT, "kzg-setup-powersoftau_amd"))
+    from kzgpot import dist as KD
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "_build", "libkzgpot_oracle.so"))
+    lo, hi = KD.shard_bounds(n, rank, world)
+    m = hi - lo
+    out = ctypes.create_string_buffer(m * 96)
+    fb = ctypes.c_int64(-1)
+    r = lib.oracle_g1_decompress(data[lo * 48: hi * 48], ctypes.c_size_t(m), out, 0, ctypes.byref(fb), None, 1, 1)
+    key = KD.NO_BAD if r == 0 else ((fb.value << 8) | (-r))
+    gkey = KD.allreduce_min_key(KD.key_with_offset(key, lo), "cpu")
+    local = torch.frombuffer(bytearray(out.raw), dtype=torch.uint8)
+    full = KD.gather_shards(local, world)
+    if rank == 0:
+        q.put((bytes(full.numpy()), gkey))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_sharded_decode_and_gather(oracle_lib, world):
+    vecs = [v for v in golden("g1_decompress") if v["check"] and v["status"] == 0][:32]
+    assert len(vecs) == 32
+    bad = golden("g1_decompress")
+    bad_vec = next(v for v in bad if v["status"] == 5)
+    data = bytearray(b"".join(bytes.fromhex(v["in"]) for v in vecs))
+    bad_index = 21  # in rank 1's shard
+    data[bad_index * 48:(bad_index + 1) * 48] = bytes.fromhex(bad_vec["in"])
+    n = len(vecs)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, bytes(data), n, bad_index, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    full, gkey = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # single-process reference
+    out = ctypes.create_string_buffer(n * 96)
+    fb = ctypes.c_int64(-1)
+    r = oracle_lib.oracle_g1_decompress(bytes(data), ctypes.c_size_t(n), out, 0, ctypes.byref(fb), None, 1, 1)
+    assert full == out.raw
+    assert r == -5 and fb.value == bad_index
+    assert gkey == (bad_index << 8) | 5
+
+
+def test_shard_bounds_cover():
+    from kzgpot import dist as KD
+
+    for n in (0, 1, 7, 1 << 16, (1 << 22) - 1):
+        for world in (1, 2, 4, 8):
+            spans = [KD.shard_bounds(n, r, world) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            for (a, b), (c, d) in zip(spans, spans[1:]):
+                assert b == c and a <= b
+    assert KD.key_with_offset(KD.NO_BAD, 5) == KD.NO_BAD
+    assert KD.key_with_offset((3 << 8) | 5, 100) == (103 << 8) | 5

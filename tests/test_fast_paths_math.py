@@ -1,0 +1,108 @@
+"""The GPU replaces two reference algorithms by faster EQUIVALENT ones; this pins the
+equivalence on the CPU, independently of the kernels.
+
+1. Subgroup test. Reference: [r]P == O by ark double-and-add. GPU: G1 φ(P) == [-u²]P,
+   G2 ψ(P) == [u]P. Both accept exactly the order-r subgroup among points ON the curve:
+   * G1: on E(Fp)[ℓ] for every ℓ | h1 we have u ≡ 1 (mod ℓ), so φ + [u²] acts as φ + 1; an
+     eigenvalue -1 of φ would need (-1)² + (-1) + 1 ≡ 0 (mod ℓ) — impossible.
+   * G2: ψ satisfies ψ² - tψ + p = 0; an eigenvector with eigenvalue u forces
+     ℓ | u² - tu + p = p - u = h1·r, but gcd(h2, h1·r) = 1.
+2. Fp2 square root. Reference: Algorithm 9 (two Fp2 exponentiations, data-dependent branches).
+   GPU: a norm-based root from two Fp exponentiations. Any root is fine because the sign rule
+   normalises it; accept/reject must agree (a is a square in Fp2 iff N(a) is a square in Fp).
+"""
+import math
+import random
+
+import kzgpot_oracle as O
+
+P = O.P
+
+
+def g1_fast(pt):
+    """Restatement of in_subgroup_fast_g1 (curve.hpp) on an affine on-curve point."""
+    beta = 0x5F19672FDF76CE51BA69C6076A0F77EADDB3A93BE6F89688DE17D813620A00022E01FFFFFFFEFFFE
+    q = O.g1_mul(O.g1_mul(pt, -O.U_PARAM), -O.U_PARAM)  # [|u|]([|u|]P) = [u²]P
+    return q == (beta * pt[0] % P, (-pt[1]) % P)
+
+
+def g2_fast(pt):
+    """Restatement of in_subgroup_fast_g2: [|u|]P == -ψ(P)."""
+    cx = O.fp2_inv(O.fp2_pow((1, 1), (P - 1) // 3))
+    cy = O.fp2_inv(O.fp2_pow((1, 1), (P - 1) // 2))
+    psi = (O.fp2_mul(O.fp2_conj(pt[0]), cx), O.fp2_mul(O.fp2_conj(pt[1]), cy))
+    return O.g2_mul(pt, -O.U_PARAM) == (psi[0], O.fp2_neg(psi[1]))
+
+
+def g1_ref(pt):
+    return O.ark_mul_bits_is_zero(O._Fp, pt[0], pt[1], False)
+
+
+def g2_ref(pt):
+    return O.ark_mul_bits_is_zero(O._Fp2, pt[0], pt[1], False)
+
+
+def test_soundness_arguments():
+    h1_primes = [3, 11, 10177, 859267, 52437899]
+    assert math.prod(p ** (1 if p == 3 else 2) for p in h1_primes) == O.H1
+    for ell in h1_primes:
+        assert (O.U_PARAM - 1) % ell == 0             # u ≡ 1 (mod ℓ)
+        assert (1 - 1 + 1) % ell != 0                 # -1 is never a root of x² + x + 1
+    t = O.U_PARAM + 1
+    assert O.P - O.U_PARAM == O.H1 * O.R_ORDER        # u² - t u + p = p - u
+    assert math.gcd(O.H2, O.H1 * O.R_ORDER) == 1
+    assert (O.U_PARAM * O.U_PARAM - t * O.U_PARAM + O.P) == O.P - O.U_PARAM
+
+
+def test_endomorphisms_on_generators():
+    assert g1_fast(O.G1_GEN) and g1_ref(O.G1_GEN)
+    assert g2_fast(O.G2_GEN) and g2_ref(O.G2_GEN)
+
+
+def test_fast_equals_ref_on_adversarial_points():
+    from golden.make_golden import small_order_g1, small_order_g2
+
+    rng = random.Random(7)
+    cases1 = [O.g1_mul(O.G1_GEN, rng.randrange(1, O.R_ORDER)) for _ in range(4)]
+    cases1 += [O.g1_random_on_curve(rng) for _ in range(4)]
+    for ell in (3, 11, 10177):
+        t = small_order_g1(rng, ell)
+        cases1 += [t, O.g1_add(O.g1_mul(O.G1_GEN, rng.randrange(1, O.R_ORDER)), t)]
+    for pt in cases1:
+        assert g1_fast(pt) == g1_ref(pt)
+    cases2 = [O.g2_mul(O.G2_GEN, rng.randrange(1, O.R_ORDER)) for _ in range(2)]
+    cases2 += [O.g2_random_on_curve(rng) for _ in range(2)]
+    t = small_order_g2(rng, 13)
+    cases2 += [t, O.g2_add(O.g2_mul(O.G2_GEN, 5), t)]
+    for pt in cases2:
+        assert g2_fast(pt) == g2_ref(pt)
+
+
+def fp2_sqrt_norm(a):
+    """Restatement of fp2_sqrt (codec_kernels.hip)."""
+    a0, a1 = a
+    nrm = (a0 * a0 + a1 * a1) % P
+    gam = pow(nrm, (P - 3) // 4, P) * nrm % P
+    ok1 = gam * gam % P == nrm
+    inv2 = pow(2, P - 2, P)
+    d = (a0 + gam) * inv2 % P
+    if d == 0:
+        d = a0
+    t = pow(d, (P - 3) // 4, P)
+    s = t * d % P
+    h = a1 * t % P * inv2 % P
+    y = (s, h) if s * s % P == d else ((-h) % P, s)
+    return y if ok1 and O.fp2_sqr(y) == (a0 % P, a1 % P) else None
+
+
+def test_fp2_sqrt_equivalence():
+    rng = random.Random(11)
+    cases = [(0, 0), (1, 0), (P - 1, 0), (0, 1), (0, P - 1), (4, 0), (5, 0), (0, 7)]
+    cases += [(rng.randrange(P), rng.randrange(P)) for _ in range(60)]
+    cases += [(rng.randrange(P), 0) for _ in range(10)] + [(0, rng.randrange(P)) for _ in range(10)]
+    for a in cases:
+        ref = O.fq2_sqrt(a)
+        got = fp2_sqrt_norm(a)
+        assert (ref is None) == (got is None), a
+        if ref is not None:
+            assert got in (ref, O.fp2_neg(ref))

@@ -1,0 +1,97 @@
+"""Full-size (BASELINE config 4) parity through size-independent properties: the GPU generator
+emits each point's compressed encoding AND the ark bytes it must decode to, so decode(encode(P))
+is checked byte-for-byte on all 2^27 G1 + 2^16 G2 points; plus fast-vs-reference subgroup mode
+agreement, device-API statuses and a C-oracle spot check of the generator itself."""
+import ctypes
+
+import pytest
+
+from conftest import oracle_run
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev(gpu):
+    import torch
+
+    from kzgpot import device as D
+
+    return torch, D
+
+
+def test_config4_round_trip_full_size(dev):
+    torch, D = dev
+    cuda = torch.device("cuda", 0)
+    n1, n2 = 1 << 27, 1 << 16
+    comp2, exp2 = D.synth("g2", 11, 0, n2, cuda)
+    out2 = torch.empty(n2 * 192, dtype=torch.uint8, device=cuda)
+    key = torch.empty(1, dtype=torch.int64, device=cuda)
+    D.codec_dev("g2_decompress", comp2, out2, key)
+    assert D.read_key(key) == (1 << 64) - 1
+    assert torch.equal(out2, exp2)
+    del comp2, exp2, out2
+    comp1, exp1 = D.synth("g1", 10, 0, n1, cuda)
+    out1 = torch.empty(n1 * 96, dtype=torch.uint8, device=cuda)
+    D.codec_dev("g1_decompress", comp1, out1, key)
+    assert D.read_key(key) == (1 << 64) - 1
+    assert torch.equal(out1, exp1)
+    # ~half the points carry the "greatest" flag
+    frac = (comp1.view(-1, 48)[:, 0] & 0x20).ne(0).float().mean().item()
+    assert 0.45 < frac < 0.55
+
+
+def test_generator_matches_oracle(dev, oracle_lib):
+    torch, D = dev
+    cuda = torch.device("cuda", 0)
+    comp, exp = D.synth("g1", 77, 123456, 512, cuda)
+    data = bytes(comp.cpu().numpy())
+    out, st, fb, r = oracle_run(oracle_lib, "g1_decompress", data, 512)
+    assert r == 0 and out == bytes(exp.cpu().numpy())
+    comp, exp = D.synth("g2", 78, 99, 16, cuda)
+    out, st, fb, r = oracle_run(oracle_lib, "g2_decompress", bytes(comp.cpu().numpy()), 16)
+    assert r == 0 and out == bytes(exp.cpu().numpy())
+
+
+def test_fast_and_ref_modes_agree(dev):
+    torch, D = dev
+    cuda = torch.device("cuda", 0)
+    n = 1 << 16
+    comp, exp = D.synth("g1", 5, 0, n, cuda)
+    # corrupt every 97th point's x (keeps the flags): mostly non-residues or off-subgroup points
+    v = comp.view(-1, 48)
+    v[::97, 40] ^= 0x5A
+    outs, stats = [], []
+    for flags in (0, 2):
+        out = torch.empty(n * 96, dtype=torch.uint8, device=cuda)
+        st = torch.empty(n, dtype=torch.uint8, device=cuda)
+        key = torch.empty(1, dtype=torch.int64, device=cuda)
+        D.codec_dev("g1_decompress", comp, out, key, flags=flags, d_status=st)
+        outs.append(out)
+        stats.append(st)
+    assert torch.equal(stats[0], stats[1]) and torch.equal(outs[0], outs[1])
+    bad = stats[0].ne(0)
+    assert bad.sum().item() == (n + 96) // 97
+    assert torch.equal(outs[0].view(-1, 96)[~bad], exp.view(-1, 96)[~bad])
+
+
+def test_dev_api_key_decoding(dev, gpu):
+    torch, D = dev
+    cuda = torch.device("cuda", 0)
+    comp, _ = D.synth("g1", 1, 0, 1000, cuda)
+    comp.view(-1, 48)[777, 0] &= 0x7F
+    comp.view(-1, 48)[900, 0] &= 0x7F
+    out = torch.empty(1000 * 96, dtype=torch.uint8, device=cuda)
+    key = torch.empty(1, dtype=torch.int64, device=cuda)
+    D.codec_dev("g1_decompress", comp, out, key)
+    k = D.read_key(key)
+    fb = ctypes.c_int64()
+    from kzgpot import _lib
+
+    assert _lib.load().kzgpot_decode_bad_key(k, ctypes.byref(fb)) == -1 and fb.value == 777
+
+
+def test_smoke_entry(gpu):
+    import __graft_entry__
+
+    __graft_entry__.smoke()

@@ -1,0 +1,151 @@
+"""GPU parity: the HIP codec (through the C ABI) against the oracle — bit-exact bytes and
+identical accept/reject on every vector, in both subgroup modes."""
+import ctypes
+import hashlib
+import json
+import os
+import random
+
+import pytest
+
+from conftest import GOLDEN, golden, oracle_run
+
+pytestmark = pytest.mark.gpu
+
+OPS = [("g1_decompress", 48, 96), ("g2_decompress", 96, 192), ("g1_transcode", 96, 96), ("g2_transcode", 192, 192)]
+
+
+@pytest.mark.parametrize("op,rin,rout", OPS)
+@pytest.mark.parametrize("mode", [0, 2], ids=["fast", "ref"])
+def test_golden_vectors_one_by_one(gpu, op, rin, rout, mode):
+    for v in golden(op):
+        flags = mode | (0 if v["check"] else gpu.NO_SUBGROUP_CHECK)
+        r = gpu.run_codec(op, bytes.fromhex(v["in"]), flags, want_status=True)
+        assert r.status[0] == v["status"], v["note"]
+        want = bytes.fromhex(v["out"]) if v["out"] else bytes(rout)
+        assert r.out == want, v["note"]
+        assert r.ret == -v["status"] and r.first_bad == (0 if v["status"] else -1)
+
+
+@pytest.mark.parametrize("op,rin,rout", OPS)
+def test_golden_vectors_batched(gpu, oracle_lib, op, rin, rout):
+    vecs = [v for v in golden(op) if v["check"]]
+    data = b"".join(bytes.fromhex(v["in"]) for v in vecs)
+    n = len(vecs)
+    r = gpu.run_codec(op, data, 0, want_status=True)
+    out, st, fb, ret = oracle_run(oracle_lib, op, data, n)
+    assert r.out == out and r.status == st and r.first_bad == fb and r.ret == ret
+
+
+def _random_stream(oracle_lib, n, seed, neg_every=0):
+    """n compressed G1 points [k]G (C oracle) with optional negatives sprinkled in."""
+    rng = random.Random(seed)
+    scal = b"".join(rng.randrange(1, 1 << 255).to_bytes(32, "big") for _ in range(n))
+    comp = ctypes.create_string_buffer(n * 48)
+    ark = ctypes.create_string_buffer(n * 96)
+    oracle_lib.oracle_g1_scalar_mul_encode(scal, ctypes.c_size_t(n), comp, ark)
+    data = bytearray(comp.raw)
+    if neg_every:
+        negs = [bytes.fromhex(v["in"]) for v in golden("g1_decompress") if v["status"] and v["check"]]
+        for i in range(neg_every // 2, n, neg_every):
+            data[i * 48:(i + 1) * 48] = negs[rng.randrange(len(negs))]
+    return bytes(data), ark.raw
+
+
+@pytest.mark.parametrize("n", [1, 63, 255, 256, 257, 1000, 4099])
+def test_random_g1_ragged_sizes(gpu, oracle_lib, n):
+    data, ark = _random_stream(oracle_lib, n, seed=n)
+    r = gpu.g1_decompress(data, want_status=True)
+    assert r.ret == 0 and r.first_bad == -1
+    assert r.out == ark
+
+
+def test_empty_input(gpu):
+    for op, rin, _ in OPS:
+        r = gpu.run_codec(op, b"", 0, want_status=True)
+        assert r.ret == 0 and r.out == b"" and r.first_bad == -1
+
+
+@pytest.mark.parametrize("mode", [0, 2], ids=["fast", "ref"])
+def test_mixed_stream_matches_oracle(gpu, oracle_lib, mode):
+    n = 3000
+    data, _ = _random_stream(oracle_lib, n, seed=99 + mode, neg_every=37)
+    r = gpu.g1_decompress(data, flags=mode, want_status=True)
+    out, st, fb, ret = oracle_run(oracle_lib, "g1_decompress", data, n)
+    assert r.status == st
+    assert r.out == out
+    assert (r.ret, r.first_bad) == (ret, fb)
+
+
+def test_no_subgroup_check_mode(gpu, oracle_lib):
+    n = 2000
+    data, _ = _random_stream(oracle_lib, n, seed=5, neg_every=41)
+    r = gpu.g1_decompress(data, flags=gpu.NO_SUBGROUP_CHECK, want_status=True)
+    out, st, fb, ret = oracle_run(oracle_lib, "g1_decompress", data, n, flags=1)
+    assert r.status == st and r.out == out and (r.ret, r.first_bad) == (ret, fb)
+
+
+def test_chunked_host_path_first_bad(gpu, oracle_lib):
+    """> 2^22 points exercise the host API's chunk loop; a bad point in the second chunk must be
+    reported with its global index."""
+    base, ark = _random_stream(oracle_lib, 4096, seed=3)
+    n = (1 << 22) + 4096
+    reps = n // 4096
+    data = bytearray(base * reps)
+    bad_at = (1 << 22) + 17
+    data[bad_at * 48] &= 0x7F
+    r = gpu.g1_decompress(bytes(data), want_status=True)
+    assert r.ret == -1 and r.first_bad == bad_at
+    assert r.status[bad_at] == 1 and r.status.count(0) == n - 1
+    assert r.out[:4096 * 96] == ark and r.out[bad_at * 96:(bad_at + 1) * 96] == bytes(96)
+
+
+def test_transcript_config1(gpu):
+    meta = json.load(open(os.path.join(GOLDEN, "transcript_n1024.json")))
+    tr = open(os.path.join(GOLDEN, "transcript_n1024.bin"), "rb").read()
+    kgz = gpu.preprocess_buffer(tr, 10, gpu.MODE_KZG)
+    fast = gpu.preprocess_buffer(tr, 10, gpu.MODE_FASTKZG)
+    assert hashlib.blake2b(kgz).hexdigest() == meta["kgz_blake2b"]
+    assert hashlib.blake2b(fast).hexdigest() == meta["fastkgz_blake2b"]
+
+
+def test_transcript_file_api_and_rejections(gpu, tmp_path):
+    meta = json.load(open(os.path.join(GOLDEN, "transcript_n1024.json")))
+    src = os.path.join(GOLDEN, "transcript_n1024.bin")
+    out = tmp_path / "kzg_setup"
+    gpu.preprocess_kgz(src, str(out), n_log2=10)
+    assert hashlib.blake2b(out.read_bytes()).hexdigest() == meta["kgz_blake2b"]
+    tr = bytearray(open(src, "rb").read())
+    n = 1024
+    # τG2[7] with x.c0 >= p (section 1)
+    off = 64 + (2 * n - 1) * 48 + 7 * 96
+    tr[off + 48:off + 96] = b"\xff" * 48
+    with pytest.raises(gpu.KzgPotError) as e:
+        gpu.preprocess_buffer(bytes(tr), 10)
+    assert e.value.code == -3 and e.value.section == 1 and e.value.first_bad == 7
+    with pytest.raises(gpu.KzgPotError) as e:
+        gpu.preprocess_buffer(bytes(tr[:-5]), 10)
+    assert e.value.code == -103
+    # βτG1 infinity: legal in kgz (decompress-only section), rejected by fastkgz (read_g1 panics)
+    tr = bytearray(open(src, "rb").read())
+    off = 64 + (2 * n - 1) * 48 + n * 96 + n * 48 + 3 * 48
+    tr[off:off + 48] = bytes([0xC0]) + bytes(47)
+    kgz = gpu.preprocess_buffer(bytes(tr), 10, gpu.MODE_KZG)
+    assert hashlib.blake2b(kgz).hexdigest() == meta["kgz_blake2b"]
+    with pytest.raises(gpu.KzgPotError) as e:
+        gpu.preprocess_buffer(bytes(tr), 10, gpu.MODE_FASTKZG)
+    assert e.value.code == -7 and e.value.section == 3 and e.value.first_bad == 3
+
+
+def test_read_g1_read_g2_mirror(gpu):
+    import io
+
+    v1 = [v for v in golden("g1_transcode") if v["status"] == 0]
+    stream = io.BytesIO(b"".join(bytes.fromhex(v["in"]) for v in v1))
+    assert gpu.read_g1(stream, count=len(v1)) == b"".join(bytes.fromhex(v["out"]) for v in v1)
+    v2 = [v for v in golden("g2_transcode") if v["status"] == 0]
+    stream = io.BytesIO(b"".join(bytes.fromhex(v["in"]) for v in v2))
+    assert gpu.read_g2(stream, count=len(v2)) == b"".join(bytes.fromhex(v["out"]) for v in v2)
+    bad = next(v for v in golden("g1_transcode") if v["status"] == 5)
+    with pytest.raises(gpu.KzgPotError):
+        gpu.read_g1(io.BytesIO(bytes.fromhex(bad["in"])))

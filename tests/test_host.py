@@ -1,0 +1,80 @@
+"""Host-side checks that need no GPU: the C ABI library loads and exports every symbol the
+public header declares, host-only helpers return the reference's sizes, the constants header is
+reproducible, and compute calls FAIL LOUDLY without a GPU (no CPU fallback on the product path)."""
+import ctypes
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import PKG, ROOT
+
+
+def test_library_exports_header_symbols(kzgpot_mod):
+    from kzgpot import _lib
+
+    lib = _lib.load()
+    syms = _lib.header_symbols()
+    assert len(syms) >= 20
+    missing = [s for s in syms if not hasattr(lib, s)]
+    assert not missing, missing
+    assert set(_lib.SIGNATURES) == set(syms)
+
+
+def test_synth_library_exports():
+    from kzgpot import device
+
+    if not os.path.exists(device.SYNTH_PATH):
+        subprocess.run(["make", "-C", PKG, "-j", "8"], check=True)
+    lib = ctypes.CDLL(device.SYNTH_PATH)
+    assert hasattr(lib, "kzgpot_synth_g1_dev") and hasattr(lib, "kzgpot_synth_g2_dev")
+
+
+def test_sizes_match_reference(kzgpot_mod):
+    k = kzgpot_mod
+    assert k.contribution_size(21) == 603_981_040          # preprocess-kgz.rs:83
+    assert k.output_size(21, k.MODE_KZG) == 603_980_256     # preprocess-kgz.rs:187-194
+    assert k.output_size(21, k.MODE_FASTKZG) == 1_006_633_248
+    assert k.TAU_POWERS_G1_LENGTH == (1 << 22) - 1
+
+
+def test_status_names(kzgpot_mod):
+    k = kzgpot_mod
+    assert k.status_name(-5) == "NotInSubgroup"
+    assert k.status_name(-101) == "DeviceError"
+    assert k.status_name(0) == "ok"
+    assert "gfx950" in k.version()
+
+
+def test_constants_header_is_reproducible(tmp_path):
+    hdr = os.path.join(PKG, "csrc", "bls12_381_consts.hpp")
+    before = open(hdr).read()
+    subprocess.run([sys.executable, os.path.join(ROOT, "tools", "gen_constants.py")], check=True,
+                   capture_output=True)
+    assert open(hdr).read() == before
+
+
+@pytest.mark.skipif(os.path.exists("/dev/kfd") and os.access("/dev/kfd", os.R_OK), reason="a GPU is present")
+def test_no_cpu_fallback_without_gpu(kzgpot_mod):
+    k = kzgpot_mod
+    assert k.device_count() == 0
+    enc = bytes.fromhex("97f1d3a73197d7942695638c4fa9ac0fc3688c4f9774b905a14e3a3f171bac586c55e83ff97a1aeffb3af00adb22c6bb")
+    with pytest.raises(k.KzgPotError) as e:
+        k.g1_decompress(enc)
+    assert e.value.code == -101
+    with pytest.raises(k.KzgPotError):
+        k.preprocess_buffer(bytes(k.contribution_size(2)), 2)
+
+
+def test_download_stub_has_no_network(kzgpot_mod, tmp_path):
+    k = kzgpot_mod
+    with pytest.raises(k.KzgPotError) as e:
+        k.download_kzg_setup(True, path=str(tmp_path / "absent"))
+    assert e.value.code == -105
+    p = tmp_path / "kzg_setup"
+    p.write_bytes(b"not the setup")
+    k.download_kzg_setup(False, path=str(p))  # existing file, no digest check: accepted (lib.rs:133)
+    with pytest.raises(k.KzgPotError) as e:
+        k.download_kzg_setup(True, path=str(p))
+    assert e.value.code == -104

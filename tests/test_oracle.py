@@ -1,0 +1,135 @@
+"""The oracle is pinned before anything is compared against it (CPU only).
+
+Anchors (the reference ships no vectors for this path — SURVEY.md §4, §8c):
+  * BLS12-381 spec constants: generators on the curve, of order r, with their well-known
+    zcash/pairing compressed encodings (every real transcript's τG1[0] / τG2[0] equals them);
+  * the ark ↔ pairing byte identity for finite points;
+  * agreement of two independent restatements (pure Python, C) on every golden vector and on the
+    N = 2^10 transcript pipelines;
+  * the reference's own constants (digests, sizes) reproduced.
+"""
+import hashlib
+import json
+import os
+
+import kzgpot_oracle as O
+import pytest
+
+from conftest import GOLDEN, golden, oracle_run
+
+G1_GEN_COMPRESSED = ("97f1d3a73197d7942695638c4fa9ac0fc3688c4f9774b905a14e3a3f171bac586c55e83ff97a1aeffb3af00adb22c6bb")
+G2_GEN_COMPRESSED = ("93e02b6052719f607dacd3a088274f65596bd0d09920b61ab5da61bbdc7f5049334cf11213945d57e5ac7d055d042b7e"
+                     "024aa2b2f08f0a91260805272dc51051c6e47ad4fa403b02b4510b647ae3d1770bac0326a805bbefd48056c8c121bdb8")
+
+
+def test_spec_constants():
+    assert O.P.bit_length() == 381 and O.P % 4 == 3
+    assert O.R_ORDER.bit_length() == 255
+    t = O.U_PARAM + 1
+    assert O.P + 1 - t == O.H1 * O.R_ORDER           # #E(Fp)
+    assert O.H1 == (O.U_PARAM - 1) ** 2 // 3
+    assert O.g1_on_curve(O.G1_GEN) and O.g2_on_curve(O.G2_GEN)
+    assert O.g1_mul(O.G1_GEN, O.R_ORDER) is None
+    assert O.g2_mul(O.G2_GEN, O.R_ORDER) is None
+
+
+def test_generator_encodings():
+    assert O.pairing_g1_compress(O.G1_GEN).hex() == G1_GEN_COMPRESSED
+    assert O.pairing_g2_compress(O.G2_GEN).hex() == G2_GEN_COMPRESSED
+    st, pt = O.pairing_g1_decompress(bytes.fromhex(G1_GEN_COMPRESSED))
+    assert st == 0 and pt == O.G1_GEN
+    st, pt = O.pairing_g2_decompress(bytes.fromhex(G2_GEN_COMPRESSED))
+    assert st == 0 and pt == O.G2_GEN
+
+
+def test_ark_is_byte_reversed_pairing():
+    pt = O.g1_mul(O.G1_GEN, 0xDEADBEEF)
+    un = O.pairing_g1_uncompressed(pt)
+    st, ark = O.g1_transcode_point(un)
+    assert st == 0 and ark == un[0:48][::-1] + un[48:96][::-1]
+    q = O.g2_mul(O.G2_GEN, 0xC0FFEE)
+    un = O.pairing_g2_uncompressed(q)
+    st, ark = O.g2_transcode_point(un)
+    assert st == 0 and ark == un[48:96][::-1] + un[0:48][::-1] + un[144:192][::-1] + un[96:144][::-1]
+
+
+def test_contribution_size_matches_reference():
+    # preprocess-kgz.rs:83 checks 603,981,040 at N = 2^21; output sizes from preprocess-{kgz,fastkgz}.rs
+    assert O.powersoftau_contribution_size(1 << 21) == 603_981_040
+    n = 1 << 21
+    assert (2 * n - 1) * 96 + n * 96 + 576 == 603_980_256
+    assert (2 * n - 1) * 96 + n * 96 + 2 * 192 + n * 192 == 1_006_633_248
+
+
+@pytest.mark.parametrize("name,fn", [("g1_decompress", O.g1_decompress_point), ("g2_decompress", O.g2_decompress_point)])
+def test_python_oracle_reproduces_golden(name, fn):
+    for v in golden(name)[::3]:  # the fixtures were produced by this oracle; re-derive a third
+        st, out = fn(bytes.fromhex(v["in"]), check=v["check"])
+        assert st == v["status"], v["note"]
+        assert (out.hex() if out else None) == v["out"], v["note"]
+
+
+@pytest.mark.parametrize("name,rin", [("g1_decompress", 48), ("g2_decompress", 96), ("g1_transcode", 96),
+                                      ("g2_transcode", 192)])
+def test_c_oracle_matches_golden(oracle_lib, name, rin):
+    for v in golden(name):
+        data = bytes.fromhex(v["in"])
+        flags = 0 if v["check"] else 1
+        out, st, fb, r = oracle_run(oracle_lib, name, data, 1, flags)
+        assert st[0] == v["status"], v["note"]
+        if v["out"] is None:
+            assert out == bytes(len(out)), v["note"]
+        else:
+            assert out.hex() == v["out"], v["note"]
+
+
+def test_c_oracle_batch_first_bad(oracle_lib):
+    vecs = golden("g1_decompress")
+    data = b"".join(bytes.fromhex(v["in"]) for v in vecs if v["check"])
+    want = [v["status"] for v in vecs if v["check"]]
+    out, st, fb, r = oracle_run(oracle_lib, "g1_decompress", data, len(want))
+    assert list(st) == want
+    first = next(i for i, s in enumerate(want) if s)
+    assert fb == first and r == -want[first]
+
+
+def test_transcript_pipelines(oracle_lib):
+    """Config 1: the N = 2^10 response transcript through both reference pipelines."""
+    import ctypes
+
+    meta = json.load(open(os.path.join(GOLDEN, "transcript_n1024.json")))
+    tr = open(os.path.join(GOLDEN, "transcript_n1024.bin"), "rb").read()
+    assert hashlib.blake2b(tr).hexdigest() == meta["transcript_blake2b"]
+    for fast, key, size in ((0, "kgz_blake2b", "kgz_size"), (1, "fastkgz_blake2b", "fastkgz_size")):
+        n = oracle_lib.oracle_output_size(ctypes.c_uint64(1024), fast)
+        assert n == meta[size]
+        out = ctypes.create_string_buffer(n)
+        sec, idx = ctypes.c_int(-1), ctypes.c_int64(-1)
+        r = oracle_lib.oracle_preprocess(tr, ctypes.c_size_t(len(tr)), ctypes.c_uint64(1024), fast, out, 4,
+                                         ctypes.byref(sec), ctypes.byref(idx))
+        assert r == 0
+        assert hashlib.blake2b(out.raw).hexdigest() == meta[key]
+    # structure: kgz = τG1 ‖ ατG1 ‖ vk(g, gamma_g, h, beta_h); g = τG1[0] = the generator
+    assert bytes.fromhex(meta["kgz_head_hex"])[:96] == O.ark_g1_serialize((O.G1_GEN[0], O.G1_GEN[1], False))
+    vk = bytes.fromhex(meta["kgz_tail_hex"])
+    assert vk[:96] == O.ark_g1_serialize((O.G1_GEN[0], O.G1_GEN[1], False))
+    assert vk[192:384] == O.ark_g2_serialize((O.G2_GEN[0], O.G2_GEN[1], False))
+
+
+def test_transcript_rejections(oracle_lib):
+    """A bad point anywhere makes the reference panic; the oracle reports section and index."""
+    import ctypes
+
+    tr = bytearray(open(os.path.join(GOLDEN, "transcript_n1024.bin"), "rb").read())
+    n = 1024
+    # βτG1[5] (section 3) with bit 7 cleared: decompress error even in kgz (unchecked section)
+    off = 64 + (2 * n - 1) * 48 + n * 96 + n * 48 + 5 * 48
+    tr[off] &= 0x7F
+    out = ctypes.create_string_buffer(oracle_lib.oracle_output_size(ctypes.c_uint64(n), 0))
+    sec, idx = ctypes.c_int(-1), ctypes.c_int64(-1)
+    r = oracle_lib.oracle_preprocess(bytes(tr), ctypes.c_size_t(len(tr)), ctypes.c_uint64(n), 0, out, 2,
+                                     ctypes.byref(sec), ctypes.byref(idx))
+    assert r == -1 and sec.value == 3 and idx.value == 5
+    r = oracle_lib.oracle_preprocess(bytes(tr[:-1]), ctypes.c_size_t(len(tr) - 1), ctypes.c_uint64(n), 0, out, 2,
+                                     ctypes.byref(sec), ctypes.byref(idx))
+    assert r == -103
