@@ -53,36 +53,76 @@ KZG_DEV void mac3s(uint64_t& lo, uint32_t& hi, uint32_t x, uint32_t y) {
       : "v"(x), "s"(y));
 }
 
+// Three products (a_j b_k pairs interleaved with m_j p_k pairs) in ONE asm statement. hipcc
+// cannot see inside inline asm, so it separates consecutive SGPR-writing asm statements by an
+// s_nop; packing products cuts those nops 3-6x (+9 % Fp-mul/s at 2 waves/SIMD,
+// tools/microbench/mont_variants.hip). The mad -> addc carry hand-off inside one statement needs
+// no wait state (verified with a single wave issuing back to back).
+#define KZG_MAC_STR(x, y) "v_mad_u64_u32 %0, %1, %" #x ", %" #y ", %0\n\tv_addc_co_u32_e64 %2, %1, %2, 0, %1\n\t"
+KZG_DEV void mac3x3(uint64_t& lo, uint32_t& hi, uint32_t x0, uint32_t y0, uint32_t x1, uint32_t y1, uint32_t x2,
+                    uint32_t y2) {
+  uint64_t cc;
+  asm(KZG_MAC_STR(3, 4) KZG_MAC_STR(5, 6) KZG_MAC_STR(7, 8)
+      : "+v"(lo), "=&s"(cc), "+v"(hi)
+      : "v"(x0), "v"(y0), "v"(x1), "v"(y1), "v"(x2), "v"(y2));
+}
+KZG_DEV void mac3x2(uint64_t& lo, uint32_t& hi, uint32_t x0, uint32_t y0, uint32_t x1, uint32_t y1) {
+  uint64_t cc;
+  asm(KZG_MAC_STR(3, 4) KZG_MAC_STR(5, 6) : "+v"(lo), "=&s"(cc), "+v"(hi) : "v"(x0), "v"(y0), "v"(x1), "v"(y1));
+}
+
+// Accumulate the products x[k] * y[k], k < N, into (hi:lo), N known at compile time.
+template <int N>
+KZG_DEV void mac_run(uint64_t& lo, uint32_t& hi, const uint32_t (&x)[N], const uint32_t (&y)[N]) {
+  int k = 0;
+#pragma unroll
+  for (; k + 3 <= N; k += 3) mac3x3(lo, hi, x[k], y[k], x[k + 1], y[k + 1], x[k + 2], y[k + 2]);
+  if constexpr (N % 3 == 2) mac3x2(lo, hi, x[N - 2], y[N - 2], x[N - 1], y[N - 1]);
+  if constexpr (N % 3 == 1) mac3(lo, hi, x[N - 1], y[N - 1]);
+}
+
+// Column i of the finely-integrated product scan: all a_j b_{i-j} and m_j p_{i-j} terms except the
+// (a_i b_0, m_i p_0) pair of a low column, which the caller handles (m_i is born there).
+template <int I>
+KZG_DEV void fips_column(uint64_t& lo, uint32_t& hi, const fp& a, const fp& b, const uint32_t (&m)[12]) {
+  constexpr int J0 = I < 12 ? 0 : I - 11;
+  constexpr int J1 = I < 12 ? I - 1 : 11;
+  constexpr int N = 2 * (J1 - J0 + 1);
+  if constexpr (N > 0) {
+    uint32_t x[N], y[N];
+#pragma unroll
+    for (int j = J0; j <= J1; j++) {
+      x[2 * (j - J0)] = a.v[j];
+      y[2 * (j - J0)] = b.v[I - j];
+      x[2 * (j - J0) + 1] = m[j];
+      y[2 * (j - J0) + 1] = FP_P[I - j];
+    }
+    mac_run<N>(lo, hi, x, y);
+  }
+}
+
+template <int I>
+KZG_DEV void fips_step(uint64_t& lo, uint32_t& hi, const fp& a, const fp& b, uint32_t (&m)[12], uint32_t (&out)[12]) {
+  fips_column<I>(lo, hi, a, b, m);
+  if constexpr (I < 12) {
+    mac3(lo, hi, a.v[I], b.v[0]);
+    m[I] = (uint32_t)lo * FP_PINV;
+    mac3s(lo, hi, m[I], FP_P[0]);
+  } else {
+    out[I - 12] = (uint32_t)lo;
+  }
+  lo = (lo >> 32) | ((uint64_t)hi << 32);
+  hi = 0;
+  if constexpr (I < 23) fips_step<I + 1>(lo, hi, a, b, m, out);
+}
+
 // r = a * b * R^-1 mod p  (inputs in [0, 2p], output in [0, 1.5p))
 KZG_DEV void fp_mul(fp& r, const fp& a, const fp& b) {
   uint32_t m[12];
   uint32_t out[12];
   uint64_t lo = 0;
   uint32_t hi = 0;
-#pragma unroll
-  for (int i = 0; i < 12; i++) {
-#pragma unroll
-    for (int j = 0; j < i; j++) {
-      mac3(lo, hi, a.v[j], b.v[i - j]);
-      mac3s(lo, hi, m[j], FP_P[i - j]);
-    }
-    mac3(lo, hi, a.v[i], b.v[0]);
-    m[i] = (uint32_t)lo * FP_PINV;
-    mac3s(lo, hi, m[i], FP_P[0]);
-    lo = (lo >> 32) | ((uint64_t)hi << 32);
-    hi = 0;
-  }
-#pragma unroll
-  for (int i = 12; i < 24; i++) {
-#pragma unroll
-    for (int j = i - 11; j < 12; j++) {
-      mac3(lo, hi, a.v[j], b.v[i - j]);
-      mac3s(lo, hi, m[j], FP_P[i - j]);
-    }
-    out[i - 12] = (uint32_t)lo;
-    lo = (lo >> 32) | ((uint64_t)hi << 32);
-    hi = 0;
-  }
+  fips_step<0>(lo, hi, a, b, m, out);
 #pragma unroll
   for (int i = 0; i < 12; i++) r.v[i] = out[i];
 }
