@@ -31,7 +31,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "kzg-setup-powersoftau_amd"))
 
 HBM_PEAK_GBS = 8000.0           # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-FP_MUL_PEAK = 63.7e9            # measured 12-limb Montgomery multiplies/s, profiles/r01_intmul_microbench.txt
+FP_MUL_PEAK = 77.7e9            # measured radix-2^28 Montgomery multiplies/s (best variant), profiles/r01_mont28_microbench.txt
 FP_MUL_PER_G1 = 1510            # Fp multiplies per G1 point on the fast path
 ALG_BYTES_G1 = 144              # 48 B read + 96 B written per G1 point
 ALG_BYTES_G2 = 288
@@ -205,7 +205,7 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "u32 (381-bit Montgomery, 12 x 32-bit limbs)",
+            "dtype": "u32 (381-bit Montgomery, 14 x 28-bit limbs)",
             "data": "synthetic (GPU-generated valid subgroup points [k_i]G, 128-bit k_i; resident in HBM)",
             "config": {
                 "workload": f"config 4: 2^{args.g1_log2} G1 + 2^{args.g2_log2} G2 compressed BLS12-381 "

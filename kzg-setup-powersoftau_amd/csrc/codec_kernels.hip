@@ -44,47 +44,53 @@ KZG_DEV void report(uint64_t i, int st, unsigned long long* first_bad, uint8_t* 
 }
 
 // Hide a pointer from the optimiser so loads through it are re-issued at every use (keeps the
-// affine base point out of the register file during the scalar-multiplication loops).
+// affine base point and the raw input words out of the register file during the long chains).
 template <typename T>
 KZG_DEV const T* opaque(const T* p) {
   asm volatile("" : "+v"(p));
   return p;
 }
 
-// canonical p - c (c canonical), with p - 0 mapped to 0
-KZG_DEV void neg_canon(fp& r, const fp& c) {
-  uint32_t br = 0;
-  const bool z = fp_is_zero_canon(c);
-#pragma unroll
-  for (int i = 0; i < 12; i++) {
-    const uint32_t d = __builtin_subc(FP_P[i], c.v[i], br, &br);
-    r.v[i] = z ? 0u : d;
-  }
-}
+// ---------------------------------------------------------------- 48-B coordinates <-> words
+// A coordinate travels as 12 little-endian 32-bit words (the 384-bit integer); fp381.hpp converts
+// words <-> 14 x 28-bit limbs. Flag bits live in word 11 (bits 381..383).
+using words = uint32_t[12];
 
-KZG_DEV void store2(uint4* dst, const fp& a, const fp& b) {  // 96 B: a LE then b LE
-  dst[0] = make_uint4(a.v[0], a.v[1], a.v[2], a.v[3]);
-  dst[1] = make_uint4(a.v[4], a.v[5], a.v[6], a.v[7]);
-  dst[2] = make_uint4(a.v[8], a.v[9], a.v[10], a.v[11]);
-  dst[3] = make_uint4(b.v[0], b.v[1], b.v[2], b.v[3]);
-  dst[4] = make_uint4(b.v[4], b.v[5], b.v[6], b.v[7]);
-  dst[5] = make_uint4(b.v[8], b.v[9], b.v[10], b.v[11]);
+KZG_DEV void load_le(words& w, const uint4* src) {  // 48 little-endian bytes (ark)
+  const uint4 a = src[0], b = src[1], c = src[2];
+  w[0] = a.x, w[1] = a.y, w[2] = a.z, w[3] = a.w;
+  w[4] = b.x, w[5] = b.y, w[6] = b.z, w[7] = b.w;
+  w[8] = c.x, w[9] = c.y, w[10] = c.z, w[11] = c.w;
+}
+KZG_DEV void load_be(words& w, const uint4* src) {  // 48 big-endian bytes (pairing)
+  const uint4 a = src[0], b = src[1], c = src[2];
+  const uint32_t r[12] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w};
+#pragma unroll
+  for (int k = 0; k < 12; k++) w[k] = bswap32(r[11 - k]);
+}
+KZG_DEV void store_words(uint4* dst, const words& w) {
+  dst[0] = make_uint4(w[0], w[1], w[2], w[3]);
+  dst[1] = make_uint4(w[4], w[5], w[6], w[7]);
+  dst[2] = make_uint4(w[8], w[9], w[10], w[11]);
+}
+KZG_DEV void store_canon(uint4* dst, const fp& c) {  // canonical element -> 48 LE bytes
+  words w;
+  fp_to_words(w, c);
+  store_words(dst, w);
 }
 KZG_DEV void store_zero(uint4* dst, int n16) {
 #pragma unroll 1
   for (int k = 0; k < n16; k++) dst[k] = make_uint4(0, 0, 0, 0);
 }
-KZG_DEV void load_le(fp& r, const uint4* src) {  // 48 little-endian bytes
-  const uint4 a = src[0], b = src[1], c = src[2];
-  r.v[0] = a.x, r.v[1] = a.y, r.v[2] = a.z, r.v[3] = a.w;
-  r.v[4] = b.x, r.v[5] = b.y, r.v[6] = b.z, r.v[7] = b.w;
-  r.v[8] = c.x, r.v[9] = c.y, r.v[10] = c.z, r.v[11] = c.w;
-}
-KZG_DEV void load_be(fp& r, const uint4* src) {  // 48 big-endian bytes
-  const uint4 a = src[0], b = src[1], c = src[2];
-  const uint32_t w[12] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w};
+KZG_DEV void zero_words(words& w) {
 #pragma unroll
-  for (int k = 0; k < 12; k++) r.v[k] = bswap32(w[11 - k]);
+  for (int k = 0; k < 12; k++) w[k] = 0;
+}
+// canonical words -> Montgomery element (reduced: value < 1.002 p)
+KZG_DEV void words_to_mont(fp& r, const words& w) {
+  fp t;
+  fp_from_words(t, w);
+  fp_to_mont(r, t);
 }
 
 // ================================================================================ phase 1: G1
@@ -95,29 +101,32 @@ __global__ void __launch_bounds__(kBlock) k_g1_decompress(const uint4* __restric
   const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
   const bool checked = !(flags & KZGPOT_NO_SUBGROUP_CHECK);
-  fp x;
-  load_be(x, in + i * 3);
-  const uint32_t b0 = x.v[11] >> 24;  // first byte on the wire
-  uint32_t rest = 0;
-#pragma unroll
-  for (int k = 0; k < 11; k++) rest |= x.v[k];
-  const bool inf_clean = ((x.v[11] & 0x3fffffffu) | rest) == 0;  // copy[0] &= 0x3f; all zero?
-  x.v[11] &= 0x1fffffffu;
-
   int st = 0;
-  if (!(b0 & 0x80u)) st = 1;
-  else if (b0 & 0x40u) st = inf_clean ? (checked ? 7 : 0) : 2;
-  else if (limbs_geq_p(x.v)) st = 3;
-  const bool is_inf = (b0 & 0xc0u) == 0xc0u && st == 0;
-  const bool greatest = (b0 & 0x20u) != 0;
-
+  bool is_inf, greatest;
+  fp a;
+  {
+    words w;
+    load_be(w, in + i * 3);
+    const uint32_t b0 = w[11] >> 24;  // first byte on the wire
+    uint32_t rest = 0;
+#pragma unroll
+    for (int k = 0; k < 11; k++) rest |= w[k];
+    const bool inf_clean = ((w[11] & 0x3fffffffu) | rest) == 0;  // copy[0] &= 0x3f; all zero?
+    w[11] &= 0x1fffffffu;
+    if (!(b0 & 0x80u)) st = 1;
+    else if (b0 & 0x40u) st = inf_clean ? (checked ? 7 : 0) : 2;
+    else if (words_geq_p(w)) st = 3;
+    is_inf = (b0 & 0xc0u) == 0xc0u && st == 0;
+    greatest = (b0 & 0x20u) != 0;
+    fp t, u;
+    words_to_mont(t, w);  // x < 2^381 even when rejected: bounds hold (test_field_bounds.py)
+    fp_sqr(a, t);
+    fp_mul(a, a, t);
+    fp_set(u, FP_FOUR);
+    fp_add(a, a, u);      // x^3 + 4
+  }
   // y = (x^3 + 4)^((p+1)/4); every lane runs the same chain (wave-uniform)
-  fp a, y, t;
-  fp_to_mont(t, x);
-  fp_sqr(a, t);
-  fp_mul(a, a, t);
-  fp_set(t, FP_FOUR);
-  fp_add(a, a, t);
+  fp y, t;
   fp_pow_pm3d4(t, a);
   fp_mul(y, t, a);
   fp_sqr(t, y);
@@ -126,20 +135,25 @@ __global__ void __launch_bounds__(kBlock) k_g1_decompress(const uint4* __restric
   // sign rule (pairing get_point_from_x): keep y if (y < -y) XOR greatest, canonical order
   fp yc, nyc;
   fp_from_mont(yc, y);
-  neg_canon(nyc, yc);
+  fp_neg_canon(nyc, yc);
   const bool keep = fp_lt_canon(yc, nyc) ^ greatest;
 
   uint4* dst = out + i * 6;
   if (st == 0 && !is_inf) {
+    words w;  // re-read x rather than keep it live through the exponentiation
+    load_be(w, opaque(in) + i * 3);
+    w[11] &= 0x1fffffffu;
     fp_select(yc, keep, yc, nyc);
-    store2(dst, x, yc);
+    store_words(dst, w);
+    store_canon(dst + 3, yc);
   } else {
-    fp zx, zy;
-    fp_zero(zx);
-    fp_zero(zy);
-    if (is_inf) zy.v[0] = 1, zy.v[11] = 0x40000000u;  // ark GroupAffine::zero() = (0, 1, inf)
-    if (st && checked) zx.v[11] = kPoison;             // phase 2 zero-fills and skips it
-    store2(dst, zx, zy);
+    words zx, zy;
+    zero_words(zx);
+    zero_words(zy);
+    if (is_inf) zy[0] = 1, zy[11] = 0x40000000u;  // ark GroupAffine::zero() = (0, 1, inf)
+    if (st && checked) zx[11] = kPoison;          // phase 2 zero-fills and skips it
+    store_words(dst, zx);
+    store_words(dst + 3, zy);
   }
   report(i, st, first_bad, status);
 }
@@ -150,18 +164,18 @@ __global__ void __launch_bounds__(kBlock) k_g1_decompress(const uint4* __restric
 //   gam = sqrt(N); d = (a0 + gam)/2 (d = a0 if that is 0); t = d^((p-3)/4); s = t d
 //   s^2 == d  ->  y = (s, a1 t / 2)      else (s^2 = -d, t s = -1)  ->  y = (-a1 t / 2, s)
 // and y is accepted iff gam^2 == N and y^2 == a. Two Fp exponentiations (~920 Fp multiplies)
-// where Algorithm 9 needs two Fp2 ones (~2,700).
+// where Algorithm 9 needs two Fp2 ones (~2,700). In: a reduced; out: y reduced.
 KZG_DEV bool fp2_sqrt(fp2& y, const fp2& a) {
   fp nrm, t0, gam, d, s, h, inv2;
   fp_sqr(nrm, a.c0);
   fp_sqr(t0, a.c1);
-  fp_add(nrm, nrm, t0);
+  fp_add_nr(nrm, nrm, t0);
   fp_pow_pm3d4(t0, nrm);
   fp_mul(gam, t0, nrm);
   fp_sqr(t0, gam);
   const bool ok1 = fp_eq(t0, nrm);
   fp_set(inv2, FP_INV2);
-  fp_add(d, a.c0, gam);
+  fp_add_nr(d, a.c0, gam);
   fp_mul(d, d, inv2);
   fp_select(d, fp_is_zero(d), a.c0, d);
   fp_pow_pm3d4(t0, d);  // t
@@ -171,13 +185,26 @@ KZG_DEV bool fp2_sqrt(fp2& y, const fp2& a) {
   fp_sqr(t0, s);
   const bool case1 = fp_eq(t0, d);
   fp nh;
-  fp_neg(nh, h);
+  fp_zero(nh);
+  fp_sub_red(nh, nh, h);
   fp_select(y.c0, case1, s, nh);
   fp_select(y.c1, case1, h, s);
   fp2 y2;
   f_sqr(y2, y);
-  f_sub(y2, y2, a);
+  fp_sub_red(y2.c0, y2.c0, a.c0);
+  fp_sub_red(y2.c1, y2.c1, a.c1);
   return ok1 && f_is_zero(y2);
+}
+
+// x^3 + 4 (1 + u), reduced
+KZG_DEV void g2_rhs(fp2& r, const fp2& x) {
+  fp2 t;
+  f_sqr(t, x);
+  f_mul(r, t, x);
+  fp four;
+  fp_set(four, FP_FOUR);
+  fp_add_red(r.c0, r.c0, four);
+  fp_add_red(r.c1, r.c1, four);
 }
 
 __global__ void __launch_bounds__(kBlock) k_g2_decompress(const uint4* __restrict__ in, uint4* __restrict__ out,
@@ -187,31 +214,30 @@ __global__ void __launch_bounds__(kBlock) k_g2_decompress(const uint4* __restric
   const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
   const bool checked = !(flags & KZGPOT_NO_SUBGROUP_CHECK);
-  fp2 x;  // wire order: x.c1 ‖ x.c0
-  load_be(x.c1, in + i * 6);
-  load_be(x.c0, in + i * 6 + 3);
-  const uint32_t b0 = x.c1.v[11] >> 24;
-  uint32_t rest = x.c0.v[11];
-#pragma unroll
-  for (int k = 0; k < 11; k++) rest |= x.c1.v[k] | x.c0.v[k];
-  const bool inf_clean = ((x.c1.v[11] & 0x3fffffffu) | rest) == 0;
-  x.c1.v[11] &= 0x1fffffffu;
-
   int st = 0;
-  if (!(b0 & 0x80u)) st = 1;
-  else if (b0 & 0x40u) st = inf_clean ? (checked ? 7 : 0) : 2;
-  else if (limbs_geq_p(x.c0.v) || limbs_geq_p(x.c1.v)) st = 3;
-  const bool is_inf = (b0 & 0xc0u) == 0xc0u && st == 0;
-  const bool greatest = (b0 & 0x20u) != 0;
-
-  fp2 a, y, t;
-  fp_to_mont(t.c0, x.c0);
-  fp_to_mont(t.c1, x.c1);
-  f_sqr(a, t);
-  f_mul(a, a, t);
-  fp_set(t.c0, FP_FOUR);
-  t.c1 = t.c0;
-  f_add(a, a, t);  // x^3 + 4(1 + u)
+  bool is_inf, greatest;
+  fp2 a;
+  {
+    words w1, w0;  // wire order: x.c1 ‖ x.c0
+    load_be(w1, in + i * 6);
+    load_be(w0, in + i * 6 + 3);
+    const uint32_t b0 = w1[11] >> 24;
+    uint32_t rest = w0[11];
+#pragma unroll
+    for (int k = 0; k < 11; k++) rest |= w1[k] | w0[k];
+    const bool inf_clean = ((w1[11] & 0x3fffffffu) | rest) == 0;
+    w1[11] &= 0x1fffffffu;
+    if (!(b0 & 0x80u)) st = 1;
+    else if (b0 & 0x40u) st = inf_clean ? (checked ? 7 : 0) : 2;
+    else if (words_geq_p(w0) || words_geq_p(w1)) st = 3;
+    is_inf = (b0 & 0xc0u) == 0xc0u && st == 0;
+    greatest = (b0 & 0x20u) != 0;
+    fp2 x;
+    words_to_mont(x.c0, w0);
+    words_to_mont(x.c1, w1);
+    g2_rhs(a, x);
+  }
+  fp2 y;
   const bool on = fp2_sqrt(y, a);
   if (st == 0 && !is_inf && !on) st = 4;
 
@@ -219,30 +245,38 @@ __global__ void __launch_bounds__(kBlock) k_g2_decompress(const uint4* __restric
   fp2 yc, nyc;
   fp_from_mont(yc.c0, y.c0);
   fp_from_mont(yc.c1, y.c1);
-  neg_canon(nyc.c0, yc.c0);
-  neg_canon(nyc.c1, yc.c1);
+  fp_neg_canon(nyc.c0, yc.c0);
+  fp_neg_canon(nyc.c1, yc.c1);
   bool c1eq = true;
 #pragma unroll
-  for (int k = 0; k < 12; k++) c1eq = c1eq && (yc.c1.v[k] == nyc.c1.v[k]);
+  for (int k = 0; k < NL; k++) c1eq = c1eq && (yc.c1.v[k] == nyc.c1.v[k]);
   const bool lt = c1eq ? fp_lt_canon(yc.c0, nyc.c0) : fp_lt_canon(yc.c1, nyc.c1);
   const bool keep = lt ^ greatest;
 
   uint4* dst = out + i * 12;
   if (st == 0 && !is_inf) {
+    words w1, w0;
+    load_be(w1, opaque(in) + i * 6);
+    load_be(w0, opaque(in) + i * 6 + 3);
+    w1[11] &= 0x1fffffffu;
     fp_select(yc.c0, keep, yc.c0, nyc.c0);
     fp_select(yc.c1, keep, yc.c1, nyc.c1);
-    store2(dst, x.c0, x.c1);
-    store2(dst + 6, yc.c0, yc.c1);
+    store_words(dst, w0);
+    store_words(dst + 3, w1);
+    store_canon(dst + 6, yc.c0);
+    store_canon(dst + 9, yc.c1);
   } else {
-    fp z, zy0, zy1;
-    fp_zero(z);
-    fp_zero(zy0);
-    fp_zero(zy1);
-    if (is_inf) zy0.v[0] = 1, zy1.v[11] = 0x40000000u;  // ark zero() = ((0,0), (1,0), inf)
-    fp zx = z;
-    if (st && checked) zx.v[11] = kPoison;
-    store2(dst, zx, z);
-    store2(dst + 6, zy0, zy1);
+    words z, zx, zy0, zy1;
+    zero_words(z);
+    zero_words(zx);
+    zero_words(zy0);
+    zero_words(zy1);
+    if (is_inf) zy0[0] = 1, zy1[11] = 0x40000000u;  // ark zero() = ((0,0), (1,0), inf)
+    if (st && checked) zx[11] = kPoison;
+    store_words(dst, zx);
+    store_words(dst + 3, z);
+    store_words(dst + 6, zy0);
+    store_words(dst + 9, zy1);
   }
   report(i, st, first_bad, status);
 }
@@ -258,8 +292,7 @@ enum class Src { ArkInPlace, PairingBE };
 
 template <Src S>
 struct G1Rec {
-  // field offsets in 16-B units inside one record
-  static KZG_DEV void load_xy(fp& x, fp& y, const uint4* rec) {
+  static KZG_DEV void load_xy(words& x, words& y, const uint4* rec) {
     if constexpr (S == Src::ArkInPlace) {
       load_le(x, rec);
       load_le(y, rec + 3);
@@ -279,27 +312,31 @@ __global__ void __launch_bounds__(kBlock) k_g1_check(const uint4* __restrict__ i
   if (i >= n) return;
   const uint4* rec = (S == Src::ArkInPlace ? (const uint4*)out : in) + i * 6;
   uint4* dst = out + i * 6;
-  fp x, y;
-  G1Rec<S>::load_xy(x, y, rec);
-  if (S == Src::ArkInPlace && x.v[11] == kPoison) {  // phase 1 already rejected (and reported) it
-    store_zero(dst, 6);
-    return;
-  }
-  const uint32_t yb = y.v[11] >> 24;  // ark SWFlags: top byte of y
-  const bool fpos = yb & 0x80u, finf = yb & 0x40u;
-  y.v[11] &= 0x3fffffffu;
   int st = 0;
-  if (limbs_geq_p(x.v)) st = 3;
-  else if (fpos && finf) st = 6;
-  else if (limbs_geq_p(y.v)) st = 3;
+  bool finf;
+  {
+    words x, y;
+    G1Rec<S>::load_xy(x, y, rec);
+    if (S == Src::ArkInPlace && x[11] == kPoison) {  // phase 1 already rejected (and reported) it
+      store_zero(dst, 6);
+      return;
+    }
+    const uint32_t yb = y[11] >> 24;  // ark SWFlags: top byte of y
+    const bool fpos = yb & 0x80u;
+    finf = yb & 0x40u;
+    y[11] &= 0x3fffffffu;
+    if (words_geq_p(x)) st = 3;
+    else if (fpos && finf) st = 6;
+    else if (words_geq_p(y)) st = 3;
+  }
 
   if (st == 0 && !finf) {
     auto load = [&](fp& bx, fp& by) {
-      fp cx, cy;
+      words cx, cy;
       G1Rec<S>::load_xy(cx, cy, opaque(rec));
-      cy.v[11] &= 0x3fffffffu;
-      fp_to_mont(bx, cx);
-      fp_to_mont(by, cy);
+      cy[11] &= 0x3fffffffu;
+      words_to_mont(bx, cx);
+      words_to_mont(by, cy);
     };
     bool on_curve;
     {
@@ -322,25 +359,30 @@ __global__ void __launch_bounds__(kBlock) k_g1_check(const uint4* __restrict__ i
   if (st) {
     store_zero(dst, 6);
   } else if (S == Src::PairingBE) {
-    if (finf) y.v[11] |= 0x40000000u;  // GroupAffine::new(x, y, true) keeps x, y
-    store2(dst, x, y);
+    words x, y;
+    G1Rec<S>::load_xy(x, y, opaque(rec));
+    y[11] &= 0x3fffffffu;
+    if (finf) y[11] |= 0x40000000u;  // GroupAffine::new(x, y, true) keeps x, y
+    store_words(dst, x);
+    store_words(dst + 3, y);
   }
   report(i, st, first_bad, status);
 }
 
 template <Src S>
 struct G2Rec {
-  static KZG_DEV void load_xy(fp2& x, fp2& y, const uint4* rec) {
+  // x.c0, x.c1, y.c0, y.c1 as words
+  static KZG_DEV void load_xy(words& x0, words& x1, words& y0, words& y1, const uint4* rec) {
     if constexpr (S == Src::ArkInPlace) {  // x.c0, x.c1, y.c0, y.c1 (LE)
-      load_le(x.c0, rec);
-      load_le(x.c1, rec + 3);
-      load_le(y.c0, rec + 6);
-      load_le(y.c1, rec + 9);
+      load_le(x0, rec);
+      load_le(x1, rec + 3);
+      load_le(y0, rec + 6);
+      load_le(y1, rec + 9);
     } else {  // wire: x.c1, x.c0, y.c1, y.c0 (BE)
-      load_be(x.c1, rec);
-      load_be(x.c0, rec + 3);
-      load_be(y.c1, rec + 6);
-      load_be(y.c0, rec + 9);
+      load_be(x1, rec);
+      load_be(x0, rec + 3);
+      load_be(y1, rec + 6);
+      load_be(y0, rec + 9);
     }
   }
 };
@@ -354,42 +396,43 @@ __global__ void __launch_bounds__(kBlock) k_g2_check(const uint4* __restrict__ i
   if (i >= n) return;
   const uint4* rec = (S == Src::ArkInPlace ? (const uint4*)out : in) + i * 12;
   uint4* dst = out + i * 12;
-  fp2 x, y;
-  G2Rec<S>::load_xy(x, y, rec);
-  if (S == Src::ArkInPlace && x.c0.v[11] == kPoison) {
-    store_zero(dst, 12);
-    return;
-  }
-  const uint32_t yb = y.c1.v[11] >> 24;
-  const bool fpos = yb & 0x80u, finf = yb & 0x40u;
-  y.c1.v[11] &= 0x3fffffffu;
   int st = 0;
-  if (limbs_geq_p(x.c0.v) || limbs_geq_p(x.c1.v)) st = 3;
-  else if (limbs_geq_p(y.c0.v)) st = 3;
-  else if (fpos && finf) st = 6;
-  else if (limbs_geq_p(y.c1.v)) st = 3;
+  bool finf;
+  {
+    words x0, x1, y0, y1;
+    G2Rec<S>::load_xy(x0, x1, y0, y1, rec);
+    if (S == Src::ArkInPlace && x0[11] == kPoison) {
+      store_zero(dst, 12);
+      return;
+    }
+    const uint32_t yb = y1[11] >> 24;
+    const bool fpos = yb & 0x80u;
+    finf = yb & 0x40u;
+    y1[11] &= 0x3fffffffu;
+    if (words_geq_p(x0) || words_geq_p(x1)) st = 3;
+    else if (words_geq_p(y0)) st = 3;
+    else if (fpos && finf) st = 6;
+    else if (words_geq_p(y1)) st = 3;
+  }
 
   if (st == 0 && !finf) {
     auto load = [&](fp2& bx, fp2& by) {
-      fp2 cx, cy;
-      G2Rec<S>::load_xy(cx, cy, opaque(rec));
-      cy.c1.v[11] &= 0x3fffffffu;
-      fp_to_mont(bx.c0, cx.c0);
-      fp_to_mont(bx.c1, cx.c1);
-      fp_to_mont(by.c0, cy.c0);
-      fp_to_mont(by.c1, cy.c1);
+      words x0, x1, y0, y1;
+      G2Rec<S>::load_xy(x0, x1, y0, y1, opaque(rec));
+      y1[11] &= 0x3fffffffu;
+      words_to_mont(bx.c0, x0);
+      words_to_mont(bx.c1, x1);
+      words_to_mont(by.c0, y0);
+      words_to_mont(by.c1, y1);
     };
     bool on_curve;
     {
       fp2 xm, ym, l, r;
       load(xm, ym);
       f_sqr(l, ym);
-      f_sqr(r, xm);
-      f_mul(r, r, xm);
-      fp_set(xm.c0, FP_FOUR);
-      xm.c1 = xm.c0;
-      f_add(r, r, xm);
-      f_sub(l, l, r);
+      g2_rhs(r, xm);
+      fp_sub_red(l.c0, l.c0, r.c0);
+      fp_sub_red(l.c1, l.c1, r.c1);
       on_curve = f_is_zero(l);
     }
     bool ok;
@@ -402,9 +445,14 @@ __global__ void __launch_bounds__(kBlock) k_g2_check(const uint4* __restrict__ i
   if (st) {
     store_zero(dst, 12);
   } else if (S == Src::PairingBE) {
-    if (finf) y.c1.v[11] |= 0x40000000u;
-    store2(dst, x.c0, x.c1);
-    store2(dst + 6, y.c0, y.c1);
+    words x0, x1, y0, y1;
+    G2Rec<S>::load_xy(x0, x1, y0, y1, opaque(rec));
+    y1[11] &= 0x3fffffffu;
+    if (finf) y1[11] |= 0x40000000u;
+    store_words(dst, x0);
+    store_words(dst + 3, x1);
+    store_words(dst + 6, y0);
+    store_words(dst + 9, y1);
   }
   report(i, st, first_bad, status);
 }

@@ -1,18 +1,19 @@
 // Short-Weierstrass (a = 0) Jacobian arithmetic over Fp / Fp2 and the two subgroup tests.
 //
-//  * jac_dbl / jac_madd restate ark-ec 0.2.0 `GroupProjective::double_in_place` (dbl-2009-l,
+//  * jac_dbl / jac_madd compute ark-ec 0.2.0 `GroupProjective::double_in_place` (dbl-2009-l,
 //    COEFF_A = 0) and `add_assign_mixed` (madd-2007-bl incl. its `self.is_zero()` and equal-point
-//    branches) exactly, so `in_subgroup_ref` (= `mul_bits(r).is_zero()`, the reference's
-//    `is_in_correct_subgroup_assuming_on_curve`) returns the reference's boolean for ANY input,
-//    on the curve or not (read_g1/read_g2 never check the curve equation).
+//    branches). The formulas are re-associated for this machine — a squaring costs the same as a
+//    multiply here, so 2((X+B)^2 - A - C) becomes 4XB, (Z+H)^2 - Z^2 - H^2 becomes 2ZH, etc. — which
+//    changes no field value: every output is the same element of Fp, so `in_subgroup_ref`
+//    (= `mul_bits(r).is_zero()`, the reference's `is_in_correct_subgroup_assuming_on_curve`)
+//    returns the reference's boolean for ANY input, on the curve or not.
 //  * in_subgroup_fast_g1 / _g2 are endomorphism tests, equal to the reference's boolean for every
-//    point ON the curve (DESIGN.md §4 has the argument; tests/ check it on adversarial points):
+//    point ON the curve (tests/test_fast_paths_math.py):
 //      G1: phi(P) == [-u^2] P,  phi(x, y) = (BETA x, y)       (126 doublings instead of 254)
 //      G2: psi(P) == [u] P,     psi = untwist-Frobenius-twist (63 doublings instead of 254)
 //
-// Register pressure decides occupancy here (one point per lane, ~100+ live 32-bit limbs), so
-// formulas are ordered to retire temporaries early and the affine base point is re-loaded from
-// memory by a `Load` functor at each use instead of being held in registers across the loops.
+// Limb / value bounds of every step are annotated (bits = limb bound, v = value bound in units of
+// p) and machine-checked by tests/test_field_bounds.py, which mirrors these formulas.
 #pragma once
 #include "fp381.hpp"
 
@@ -23,45 +24,102 @@ struct jac {
   F x, y, z;
 };
 
-// ark double_in_place (a = 0). Z = 0 stays Z = 0 (Z3 = 2 Y Z), matching ark's early return in
-// everything that is observable (is_zero() reads Z only; the next add replaces X, Y).
-template <typename F>
-KZG_DEV void jac_dbl(jac<F>& p) {
-  F a, c, d, t;
-  f_sqr(a, p.x);      // A = X^2
-  f_sqr(t, p.y);      // B = Y^2
-  f_sqr(c, t);        // C = B^2
-  f_add(t, p.x, t);   // X + B
-  f_sqr(t, t);
-  f_sub(t, t, a);
-  f_sub(t, t, c);
-  f_dbl(d, t);        // D = 2((X+B)^2 - A - C)
-  f_dbl(t, a);
-  f_add(a, t, a);     // E = 3A (in a)
-  f_mul(p.z, p.z, p.y);
-  f_dbl(p.z, p.z);    // Z3 = 2 Y Z
-  f_sqr(t, a);        // F = E^2
-  f_sub(t, t, d);
-  f_sub(p.x, t, d);   // X3 = F - 2D
-  f_sub(t, d, p.x);
-  f_mul(t, t, a);     // E (D - X3)
-  f_dbl(c, c);
-  f_dbl(c, c);
-  f_dbl(c, c);
-  f_sub(p.y, t, c);   // Y3 = E (D - X3) - 8C
+// ---------------------------------------------------------------- generic helpers
+// Fp: carry-free limb-wise forms (bounds proven by tests/test_field_bounds.py).
+// Fp2 (cold G2 path): every component stays reduced (< 2p); the borrowed constant is not needed
+// and each op reduces its result, so the same formulas hold with no value drift.
+KZG_DEV void f_subk(fp& r, const fp& a, const fp& b, const uint32_t (&k)[NL]) { fp_subk_nr(r, a, b, k); }
+KZG_DEV void f_subk(fp2& r, const fp2& a, const fp2& b, const uint32_t (&)[NL]) {
+  fp_sub_red(r.c0, a.c0, b.c0);
+  fp_sub_red(r.c1, a.c1, b.c1);
+}
+template <int S>
+KZG_DEV void f_shl(fp& r, const fp& a) { fp_shl_nr<S>(r, a); }
+template <int S>
+KZG_DEV void f_shl(fp2& r, const fp2& a) {
+  r = a;
+#pragma unroll
+  for (int k = 0; k < S; k++) {
+    fp_add_red(r.c0, r.c0, r.c0);
+    fp_add_red(r.c1, r.c1, r.c1);
+  }
+}
+KZG_DEV void f_mul3(fp& r, const fp& a) { fp_mul3_nr(r, a); }
+KZG_DEV void f_mul3(fp2& r, const fp2& a) {
+  fp2 t;
+  fp_add_red(t.c0, a.c0, a.c0);
+  fp_add_red(t.c1, a.c1, a.c1);
+  fp_add_red(r.c0, t.c0, a.c0);
+  fp_add_red(r.c1, t.c1, a.c1);
+}
+KZG_DEV void f_norm(fp2& r, const fp2& a) { r = a; }
+
+// ---------------------------------------------------------------- doubling
+// Hot path (G1, 252 doublings per point). In: X, Y limbs < 2^30, Z normalized, values <= 40.
+// Out: X3, Y3 limbs < 2^30 (v <= 4.1, 3.1), Z3 normalized. No carry propagation at all.
+KZG_DEV void jac_dbl(jac<fp>& p) {
+  fp a, b, c8, d, e, t;
+  fp_sqr(a, p.x);              // A = X^2                    N
+  fp_sqr(b, p.y);              // B = Y^2                    N
+  fp_shl_nr<3>(t, b);          // 8B                        < 2^31
+  fp_mul(c8, t, b);            // 8C = 8 B^2                 N
+  fp_shl_nr<2>(t, p.x);        // 4X                        < 2^32
+  fp_mul(d, t, b);             // D = 4 X B                  N
+  fp_mul3_nr(e, a);            // E = 3A                    < 3 * 2^28
+  fp_shl_nr<1>(t, p.y);        // 2Y                        < 2^31
+  fp_mul(p.z, t, p.z);         // Z3 = 2 Y Z                 N
+  fp_sqr(a, e);                // F = E^2                    N
+  fp_shl_nr<1>(t, d);          // 2D                        < 2^29
+  fp_subk_nr(p.x, a, t, KB_8_29);  // X3 = F - 2D           < 2^30 + 2^28
+  fp_mul3_nr(t, d);            // 3D
+  fp_subk_nr(t, t, a, KB_8_28);    // D - X3 = 3D - F       < 5 * 2^28
+  fp_mul(t, e, t);             // E (D - X3)                 N
+  fp_subk_nr(p.y, t, c8, KB_8_28); // Y3 = E (D - X3) - 8C  < 2^30
 }
 
-// ark add_assign_mixed: p += (x2, y2) for a finite affine (x2, y2).
+// Generic (Fp2, cold): all values reduced (< 2p) through the Fp2 helpers above.
+template <typename F>
+KZG_DEV void jac_dbl(jac<F>& p) {
+  F a, b, c8, d, e, t;
+  f_sqr(a, p.x);
+  f_sqr(b, p.y);
+  f_shl<3>(t, b);
+  f_norm(t, t);
+  f_mul(c8, t, b);             // 8C
+  f_shl<2>(t, p.x);
+  f_norm(t, t);
+  f_mul(d, t, b);              // D = 4XB
+  f_mul3(e, a);
+  f_norm(e, e);                // E = 3A
+  f_shl<1>(t, p.y);
+  f_norm(t, t);
+  f_mul(p.z, t, p.z);          // Z3 = 2YZ
+  f_sqr(a, e);                 // F
+  f_shl<1>(t, d);
+  f_subk(p.x, a, t, KB_64_29);
+  f_norm(p.x, p.x);            // X3 = F - 2D
+  f_mul3(t, d);
+  f_subk(t, t, a, KB_16_28);
+  f_norm(t, t);                // 3D - F
+  f_mul(t, e, t);
+  f_subk(p.y, t, c8, KB_32_28);
+  f_norm(p.y, p.y);            // Y3
+}
+
+// ---------------------------------------------------------------- mixed addition (cold)
+// ark add_assign_mixed: p += (x2, y2) for a finite affine (x2, y2) (normalized, v <= 2).
+// In: X, Y limbs < 2^30, values <= 40; Z normalized. Out: normalized, values <= 64.
 template <typename F>
 KZG_DEV void jac_madd(jac<F>& p, const F& x2, const F& y2) {
   F z1z1, h, r, t;
   f_sqr(z1z1, p.z);
-  f_mul(h, x2, z1z1);
-  f_sub(h, h, p.x);   // H = U2 - X1
+  f_mul(h, x2, z1z1);          // U2
+  f_subk(h, h, p.x, KB_128_31);
+  f_norm(h, h);                // H = U2 - X1
   f_mul(t, y2, p.z);
-  f_mul(t, t, z1z1);  // S2
-  f_sub(r, t, p.y);
-  f_dbl(r, r);        // r = 2 (S2 - Y1)
+  f_mul(t, t, z1z1);           // S2
+  f_subk(r, t, p.y, KB_64_31);
+  f_norm(r, r);                // r' = S2 - Y1   (ark's r = 2 r')
   const bool z1zero = f_is_zero(p.z);
   const bool same = !z1zero && f_is_zero(h) && f_is_zero(r);
   if (__builtin_expect(z1zero || same, 0)) {
@@ -74,29 +132,36 @@ KZG_DEV void jac_madd(jac<F>& p, const F& x2, const F& y2) {
     }
     return;
   }
-  F i, j;
-  f_sqr(t, h);        // HH
-  f_add(p.z, p.z, h);
-  f_sqr(p.z, p.z);
-  f_sub(p.z, p.z, z1z1);
-  f_sub(p.z, p.z, t); // Z3 = (Z1 + H)^2 - Z1Z1 - HH
-  f_dbl(i, t);
-  f_dbl(i, i);        // I = 4 HH
-  f_mul(j, h, i);     // J = H I
-  f_mul(i, p.x, i);   // V = X1 I  (in i)
-  f_sqr(t, r);
-  f_sub(t, t, j);
-  f_sub(t, t, i);
-  f_sub(t, t, i);     // X3 = r^2 - J - 2V
-  f_mul(j, j, p.y);
-  f_dbl(j, j);        // 2 Y1 J
-  f_sub(i, i, t);
-  f_mul(i, i, r);
-  f_sub(p.y, i, j);   // Y3 = r (V - X3) - 2 Y1 J
+  F hh, j;
+  f_sqr(hh, h);                // HH
+  f_shl<1>(t, p.z);
+  f_norm(t, t);
+  f_mul(p.z, t, h);            // Z3 = 2 Z1 H  (= (Z1 + H)^2 - Z1Z1 - HH)
+  f_shl<2>(hh, hh);
+  f_norm(hh, hh);              // I = 4 HH
+  f_mul(j, h, hh);             // J = H I
+  f_mul(hh, p.x, hh);          // V = X1 I
+  f_sqr(t, r);                 // r'^2
+  f_shl<2>(t, t);              // r^2 = 4 r'^2
+  f_subk(t, t, j, KB_32_28);
+  f_shl<1>(h, hh);             // 2V
+  f_subk(t, t, h, KB_64_29);
+  f_norm(t, t);                // X3 = r^2 - J - 2V
+  f_subk(hh, hh, t, KB_128_28);
+  f_norm(hh, hh);              // V - X3
+  f_shl<1>(r, r);
+  f_norm(r, r);                // r = 2 r'
+  f_mul(hh, r, hh);            // r (V - X3)
+  f_shl<1>(h, p.y);
+  f_norm(h, h);
+  f_mul(j, h, j);              // 2 Y1 J
+  f_subk(p.y, hh, j, KB_32_28);
+  f_norm(p.y, p.y);            // Y3
   p.x = t;
 }
 
-// p += q, both Jacobian (add-2007-bl) with the O / equal-point cases handled.
+// p += q, both Jacobian (add-2007-bl) with the O / equal-point cases handled. Cold (10 per G1
+// point). In: p from jac_dbl<fp> (X, Y < 2^30), q normalized; values <= 64. Out normalized.
 template <typename F>
 KZG_DEV void jac_add(jac<F>& p, const jac<F>& q) {
   const bool pzero = f_is_zero(p.z);
@@ -104,15 +169,16 @@ KZG_DEV void jac_add(jac<F>& p, const jac<F>& q) {
   F z1z1, z2z2, u1, s1, h, r;
   f_sqr(z1z1, p.z);
   f_sqr(z2z2, q.z);
-  f_mul(u1, p.x, z2z2);
+  f_mul(u1, p.x, z2z2);        // U1
   f_mul(s1, p.y, q.z);
-  f_mul(s1, s1, z2z2);
+  f_mul(s1, s1, z2z2);         // S1
   f_mul(h, q.x, z1z1);
-  f_sub(h, h, u1);     // H = U2 - U1
+  f_subk(h, h, u1, KB_8_28);
+  f_norm(h, h);                // H = U2 - U1
   f_mul(r, q.y, p.z);
   f_mul(r, r, z1z1);
-  f_sub(r, r, s1);
-  f_dbl(r, r);         // r = 2 (S2 - S1)
+  f_subk(r, r, s1, KB_8_28);
+  f_norm(r, r);                // r' = S2 - S1
   const bool same = !pzero && !qzero && f_is_zero(h) && f_is_zero(r);
   if (__builtin_expect(pzero || qzero || same, 0)) {
     if (same)
@@ -121,24 +187,31 @@ KZG_DEV void jac_add(jac<F>& p, const jac<F>& q) {
       p = q;
     return;
   }
-  f_add(p.z, p.z, q.z);
-  f_sqr(p.z, p.z);
-  f_sub(p.z, p.z, z1z1);
-  f_sub(p.z, p.z, z2z2);
-  f_mul(p.z, p.z, h);  // Z3 = ((Z1 + Z2)^2 - Z1Z1 - Z2Z2) H
-  f_dbl(z1z1, h);
-  f_sqr(z1z1, z1z1);   // I = (2H)^2
-  f_mul(z2z2, h, z1z1);  // J = H I
-  f_mul(u1, u1, z1z1);   // V = U1 I
+  f_shl<1>(z1z1, p.z);
+  f_norm(z1z1, z1z1);
+  f_mul(z1z1, z1z1, q.z);
+  f_mul(p.z, z1z1, h);         // Z3 = 2 Z1 Z2 H
+  f_shl<1>(z1z1, h);
+  f_norm(z1z1, z1z1);
+  f_sqr(z1z1, z1z1);           // I = (2H)^2
+  f_mul(z2z2, h, z1z1);        // J = H I
+  f_mul(u1, u1, z1z1);         // V = U1 I
   f_sqr(h, r);
-  f_sub(h, h, z2z2);
-  f_sub(h, h, u1);
-  f_sub(h, h, u1);       // X3 = r^2 - J - 2V
-  f_mul(s1, s1, z2z2);
-  f_dbl(s1, s1);         // 2 S1 J
-  f_sub(u1, u1, h);
-  f_mul(u1, u1, r);
-  f_sub(p.y, u1, s1);    // Y3 = r (V - X3) - 2 S1 J
+  f_shl<2>(h, h);              // r^2 = 4 r'^2
+  f_subk(h, h, z2z2, KB_8_28);
+  f_shl<1>(z1z1, u1);
+  f_subk(h, h, z1z1, KB_64_29);
+  f_norm(h, h);                // X3 = r^2 - J - 2V
+  f_subk(u1, u1, h, KB_128_28);
+  f_norm(u1, u1);              // V - X3
+  f_shl<1>(r, r);
+  f_norm(r, r);
+  f_mul(u1, r, u1);            // r (V - X3)
+  f_shl<1>(s1, s1);
+  f_norm(s1, s1);
+  f_mul(s1, s1, z2z2);         // 2 S1 J
+  f_subk(p.y, u1, s1, KB_8_28);
+  f_norm(p.y, p.y);            // Y3
   p.x = h;
 }
 
@@ -168,17 +241,17 @@ KZG_DEV void mul_abs_u_jac(jac<F>& acc, const jac<F>& q) {
   }
 }
 
-// Jacobian (X, Y, Z) == affine (x, y)?  (X == x Z^2, Y == y Z^3, Z != 0)
+// Jacobian (X, Y, Z) == affine (x, y)?  (X == x Z^2, Y == y Z^3, Z != 0). X, Y limbs < 2^30.
 template <typename F>
 KZG_DEV bool jac_eq_affine(const jac<F>& p, const F& x, const F& y) {
   F z2, t;
   f_sqr(z2, p.z);
   f_mul(t, x, z2);
-  f_sub(t, t, p.x);
+  f_subk(t, t, p.x, KB_128_31);
   bool ok = f_is_zero(t);
   f_mul(z2, z2, p.z);
   f_mul(t, y, z2);
-  f_sub(t, t, p.y);
+  f_subk(t, t, p.y, KB_128_31);
   ok = ok && f_is_zero(t);
   return ok && !f_is_zero(p.z);
 }
@@ -230,7 +303,9 @@ KZG_DEV void g2_psi(fp2& x, fp2& y) {
   fp2 cy;
   fp_set(cy.c0, FP_PSI_CY0);
   fp_set(cy.c1, FP_PSI_CY1);
-  fp_neg(y.c1, y.c1);
+  fp zero;
+  fp_zero(zero);
+  fp_sub_red(y.c1, zero, y.c1);
   f_mul(y, y, cy);
 }
 
@@ -242,8 +317,7 @@ KZG_DEV bool in_subgroup_fast_g2(Load&& load) {
   fp2 x, y;
   load(x, y);
   g2_psi(x, y);
-  fp_neg(y.c0, y.c0);
-  fp_neg(y.c1, y.c1);
+  fp2_neg_red(y, y);
   return jac_eq_affine(q, x, y);
 }
 

@@ -43,7 +43,7 @@ KZG_DEV void f_inv(fp& r, const fp& a) {
   fp_sqr(t, t);
   fp_mul(r, t, a);
 }
-KZG_DEV void f_inv(fp2& r, const fp2& a) {  // (a0 - a1 u) / (a0^2 + a1^2)
+KZG_DEV void f_inv(fp2& r, const fp2& a) {  // (a0 - a1 u) / (a0^2 + a1^2); reduced in and out
   fp n, t;
   fp_sqr(n, a.c0);
   fp_sqr(t, a.c1);
@@ -51,7 +51,8 @@ KZG_DEV void f_inv(fp2& r, const fp2& a) {  // (a0 - a1 u) / (a0^2 + a1^2)
   f_inv(n, n);
   fp_mul(r.c0, a.c0, n);
   fp_mul(t, a.c1, n);
-  fp_neg(r.c1, t);
+  fp_zero(n);
+  fp_sub_red(r.c1, n, t);
 }
 
 template <typename F>
@@ -63,9 +64,6 @@ KZG_DEV void to_affine(F& x, F& y, const jac<F>& p) {
   f_mul(z2, z2, zi);
   f_mul(y, p.y, z2);
 }
-
-constexpr int limbs_of(const fp*) { return 12; }
-constexpr int limbs_of(const fp2*) { return 24; }
 
 template <typename F>
 KZG_DEV void store_f(uint32_t* dst, const F& a) {
@@ -111,15 +109,21 @@ KZG_DEV void canon_pair(fp& xc, fp& yc, bool& greatest, const fp& x, const fp& y
   fp_from_mont(yc, y);
   // greatest: y > p - y (pairing G1Compressed::from_affine)
   fp ny;
-  uint32_t br = 0;
-#pragma unroll
-  for (int i = 0; i < 12; i++) ny.v[i] = __builtin_subc(FP_P[i], yc.v[i], br, &br);
+  fp_neg_canon(ny, yc);
   greatest = fp_lt_canon(ny, yc);
 }
 
 KZG_DEV void store_be(uint32_t* dst, const fp& c) {  // canonical -> 48 big-endian bytes
+  uint32_t w[12];
+  fp_to_words(w, c);
 #pragma unroll
-  for (int k = 0; k < 12; k++) dst[k] = __builtin_bswap32(c.v[11 - k]);
+  for (int k = 0; k < 12; k++) dst[k] = __builtin_bswap32(w[11 - k]);
+}
+KZG_DEV void store_le(uint32_t* dst, const fp& c) {  // canonical -> 48 little-endian bytes
+  uint32_t w[12];
+  fp_to_words(w, c);
+#pragma unroll
+  for (int k = 0; k < 12; k++) dst[k] = w[k];
 }
 
 template <typename F>
@@ -161,8 +165,8 @@ __global__ void __launch_bounds__(kSynthBlock) k_synth(const uint32_t* __restric
     c[0] |= 0x80u | (greatest ? 0x20u : 0u);
     if (ark) {
       uint32_t* a = ark + i * 24;
-      store_f(a, xc);
-      store_f(a + 12, yc);
+      store_le(a, xc);
+      store_le(a + 12, yc);
     }
   } else {
     const fp2& x2 = *(const fp2*)&x;
@@ -174,17 +178,11 @@ __global__ void __launch_bounds__(kSynthBlock) k_synth(const uint32_t* __restric
     fp_from_mont(yc.c1, y2.c1);
     // greatest: y > -y lexicographically (c1 first)
     fp n0, n1;
-    uint32_t b0 = 0, b1 = 0;
-#pragma unroll
-    for (int k = 0; k < 12; k++) {
-      n0.v[k] = __builtin_subc(FP_P[k], yc.c0.v[k], b0, &b0);
-      n1.v[k] = __builtin_subc(FP_P[k], yc.c1.v[k], b1, &b1);
-    }
-    if (fp_is_zero_canon(yc.c0)) fp_zero(n0);
-    if (fp_is_zero_canon(yc.c1)) fp_zero(n1);
+    fp_neg_canon(n0, yc.c0);
+    fp_neg_canon(n1, yc.c1);
     bool c1eq = true;
 #pragma unroll
-    for (int k = 0; k < 12; k++) c1eq = c1eq && (yc.c1.v[k] == n1.v[k]);
+    for (int k = 0; k < NL; k++) c1eq = c1eq && (yc.c1.v[k] == n1.v[k]);
     const bool greatest = c1eq ? fp_lt_canon(n0, yc.c0) : fp_lt_canon(n1, yc.c1);
     uint32_t* c = comp + i * 24;
     store_be(c, xc.c1);
@@ -192,10 +190,10 @@ __global__ void __launch_bounds__(kSynthBlock) k_synth(const uint32_t* __restric
     c[0] |= 0x80u | (greatest ? 0x20u : 0u);
     if (ark) {
       uint32_t* a = ark + i * 48;
-      store_f(a, xc.c0);
-      store_f(a + 12, xc.c1);
-      store_f(a + 24, yc.c0);
-      store_f(a + 36, yc.c1);
+      store_le(a, xc.c0);
+      store_le(a + 12, xc.c1);
+      store_le(a + 24, yc.c0);
+      store_le(a + 36, yc.c1);
     }
   }
 }

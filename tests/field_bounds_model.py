@@ -1,0 +1,417 @@
+"""Exact interval model of the radix-2^28 field arithmetic in csrc/fp381.hpp and the formulas in
+csrc/curve.hpp / codec_kernels.hip — used by tests/test_field_bounds.py to PROVE (for all inputs)
+that no 64-bit column accumulator, 32-bit limb or borrowed-constant subtraction can overflow.
+
+Each value is modelled by per-limb upper bounds (exact ints) and a value upper bound (in units of
+p, a float nudged upward at every step). The functions mirror the device code one to one; keep
+them in sync.
+"""
+from __future__ import annotations
+
+import math
+import os
+import re
+from fractions import Fraction
+
+P = 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB153FFFFB9FEFFFFFFFFAAAB
+NL = 14
+LB = 28
+LM = (1 << LB) - 1
+R = 1 << (LB * NL)
+P_L = [(P >> (LB * i)) & LM for i in range(NL)]
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CONSTS = os.path.join(HERE, "..", "kzg-setup-powersoftau_amd", "csrc", "bls12_381_consts.hpp")
+
+
+def _load_consts():
+    text = open(CONSTS).read()
+    out = {}
+    for name, body in re.findall(r"static constexpr uint32_t (\w+)\[\d+\] = \{([^}]*)\}", text):
+        out[name] = [int(v.strip().rstrip("u"), 16) for v in body.split(",")]
+    return out
+
+
+C = _load_consts()
+
+
+class BoundError(AssertionError):
+    pass
+
+
+UP = 1.0 + 1e-9  # upward nudge for float value bounds
+P_OVER_R = P / R * UP
+P_TOP = P / (1 << (LB * (NL - 1))) * UP  # p / 2^364
+
+
+class V:
+    """Upper bounds: limbs[i] >= every possible limb i; val >= value / p."""
+
+    def __init__(self, limbs, val, name=""):
+        self.limbs = list(limbs)
+        self.val = float(val)
+        self.name = name
+        for i, l in enumerate(self.limbs):
+            if l >= 1 << 32:
+                raise BoundError(f"{name}: limb {i} may overflow 32 bits ({l:#x})")
+        if self.val * P >= R * (1 - 1e-6):
+            raise BoundError(f"{name}: value {float(self.val):.1f} p does not fit 392 bits")
+
+    def __repr__(self):
+        return f"V({self.name}: bits {max(l.bit_length() for l in self.limbs)}, v {float(self.val):.3f})"
+
+
+def normalized(val, name=""):
+    """A normalized value: limbs 0..12 < 2^28, top limb bounded by the value."""
+    top = int(float(val) * P_TOP) + 1
+    return V([LM] * (NL - 1) + [min(LM, top)], val, name)
+
+
+def const(limbs, name=""):
+    val = sum(l << (LB * i) for i, l in enumerate(limbs)) / P * UP
+    return V(limbs, val, name)
+
+
+def mont_output(val):
+    return normalized(val)
+
+
+def mul(a: V, b: V, name="mul"):
+    """fp_mul: FIPS with one 64-bit accumulator per column (+ the m*p chain merged in)."""
+    carry = 0
+    for i in range(2 * NL):
+        j0 = 0 if i < NL else i - (NL - 1)
+        j1 = i if i < NL else NL - 1
+        s = sum(a.limbs[j] * b.limbs[i - j] for j in range(j0, j1 + 1))
+        s += sum(LM * P_L[i - j] for j in range(j0, j1 + 1))
+        s += carry
+        if s >= 1 << 64:
+            raise BoundError(f"{name}: column {i} may reach {s.bit_length()} bits ({a!r} x {b!r})")
+        carry = s >> LB
+    val = (a.val * b.val * P_OVER_R + 1) * UP  # (ab + m p) / R < ab/R + p
+    out = normalized(val, name)
+    return out
+
+
+def add_nr(a, b, name="add"):
+    return V([x + y for x, y in zip(a.limbs, b.limbs)], (a.val + b.val) * UP, name)
+
+
+def shl(a, s, name="shl"):
+    return V([x << s for x in a.limbs], a.val * (1 << s) * UP, name)
+
+
+def mul3(a, name="mul3"):
+    return V([3 * x for x in a.limbs], a.val * 3 * UP, name)
+
+
+def subk(a, b, kname, name="subk"):
+    k = C[kname]
+    for i in range(NL):
+        if k[i] < b.limbs[i]:
+            raise BoundError(f"{name}: {kname}[{i}] = {k[i]:#x} < subtrahend limb bound {b.limbs[i]:#x} ({b!r})")
+    kv = const(k).val
+    return V([x + y for x, y in zip(a.limbs, k)], (a.val + kv) * UP, name)
+
+
+def norm(a, name="norm"):
+    for l in a.limbs:
+        if l + 16 >= 1 << 32:
+            raise BoundError(f"{name}: norm input limb too large")
+    return normalized(a.val, name)
+
+
+def canon_ok(a, name="canon"):
+    """fp_canon / fp_is_zero precondition: limbs < 2^32 - 16 (fp_norm), value < 256 p."""
+    if max(a.limbs) >= (1 << 32) - 16 or a.val >= 256:
+        raise BoundError(f"{name}: canon precondition violated {a!r}")
+
+
+def vmax(*vs):
+    return V([max(x) for x in zip(*(v.limbs for v in vs))], max(v.val for v in vs), "join")
+
+
+# ------------------------------------------------------------------------------------------
+# Fp2 (components share bounds: one V per component pair, conservatively the join)
+class V2:
+    def __init__(self, c0, c1):
+        self.c0, self.c1 = c0, c1
+
+    def j(self):
+        return vmax(self.c0, self.c1)
+
+
+def reduced(name=""):
+    return normalized(2 - 1e-7, name)  # strictly below 2p (integers: at most 2p - 1)
+
+
+def check_reduced(a, name):
+    if a.val > 2 + 1e-6 or any(l > LM for l in a.limbs[: NL - 1]) or a.limbs[NL - 1] > reduced().limbs[NL - 1]:
+        raise BoundError(f"{name}: expected a reduced (< 2p, normalized) value, got {a!r}")
+
+
+def sub_red(a, b, name="sub_red"):
+    """fp_sub_red: signed borrow chain a - b, + 2p if negative: reduced in, reduced out."""
+    check_reduced(a, name), check_reduced(b, name)
+    return reduced(name)
+
+
+def add_red(a, b, name="add_red"):
+    check_reduced(a, name), check_reduced(b, name)
+    t = add_nr(a, b, name)
+    if t.val >= 4 + 1e-6:
+        raise BoundError(f"{name}: one conditional subtraction cannot reduce {t!r}")
+    norm(t, name)
+    return reduced(name)
+
+
+def f2_mul(a: V2, b: V2, name="f2mul"):
+    for c in (a.c0, a.c1, b.c0, b.c1):
+        check_reduced(c, name)
+    t0 = mul(a.c0, b.c0, name + ".t0")
+    t1 = mul(a.c1, b.c1, name + ".t1")
+    s0 = add_nr(a.c0, a.c1)
+    s1 = add_nr(b.c0, b.c1)
+    s0 = mul(s0, s1, name + ".t2")
+    c0 = sub_red(t0, t1, name + ".c0")
+    t01 = add_red(t0, t1, name + ".t01")
+    return V2(c0, sub_red(s0, t01, name + ".c1"))
+
+
+def f2_sqr(a: V2, name="f2sqr"):
+    check_reduced(a.c0, name), check_reduced(a.c1, name)
+    s = add_nr(a.c0, a.c1)
+    d = subk(a.c0, a.c1, "KB_4_28", name + ".d")
+    t = shl(a.c0, 1)
+    c0, c1 = mul(s, d, name + ".c0"), mul(t, a.c1, name + ".c1")
+    check_reduced(c0, name), check_reduced(c1, name)
+    return V2(c0, c1)
+
+
+class Field:
+    """Dispatch generic formulas to the Fp (carry-free) or Fp2 (reduced) models."""
+
+    def __init__(self, two):
+        self.two = two
+
+    def mul(self, a, b, name="mul"):
+        return f2_mul(a, b, name) if self.two else mul(a, b, name)
+
+    def sqr(self, a, name="sqr"):
+        return f2_sqr(a, name) if self.two else mul(a, a, name)
+
+    def subk(self, a, b, k, name="subk"):
+        if self.two:
+            return V2(sub_red(a.c0, b.c0, name), sub_red(a.c1, b.c1, name))
+        return subk(a, b, k, name)
+
+    def shl(self, a, s, name="shl"):
+        if self.two:
+            for _ in range(s):
+                a = V2(add_red(a.c0, a.c0, name), add_red(a.c1, a.c1, name))
+            return a
+        return shl(a, s, name)
+
+    def mul3(self, a, name="mul3"):
+        if self.two:
+            t = V2(add_red(a.c0, a.c0, name), add_red(a.c1, a.c1, name))
+            return V2(add_red(t.c0, a.c0, name), add_red(t.c1, a.c1, name))
+        return mul3(a, name)
+
+    def norm(self, a, name="norm"):
+        return a if self.two else norm(a, name)
+
+    def canon_ok(self, a, name="canon"):
+        if self.two:
+            canon_ok(a.c0, name), canon_ok(a.c1, name)
+        else:
+            canon_ok(a, name)
+
+    def one(self):
+        o = normalized(1)
+        return V2(o, normalized(0)) if self.two else o
+
+
+# ------------------------------------------------------------------------------------------
+# formulas (mirror csrc/curve.hpp)
+def jac_dbl_fp(X, Y, Z):
+    """jac_dbl(jac<fp>&) — the hot path."""
+    a = mul(X, X, "A")
+    b = mul(Y, Y, "B")
+    t = shl(b, 3)
+    c8 = mul(t, b, "8C")
+    t = shl(X, 2)
+    d = mul(t, b, "D")
+    e = mul3(a)
+    t = shl(Y, 1)
+    z3 = mul(t, Z, "Z3")
+    a = mul(e, e, "F")
+    t = shl(d, 1)
+    x3 = subk(a, t, "KB_8_29", "X3")
+    t = mul3(d)
+    t = subk(t, a, "KB_8_28", "3D-F")
+    t = mul(e, t, "E(D-X3)")
+    y3 = subk(t, c8, "KB_8_28", "Y3")
+    return x3, y3, z3
+
+
+def jac_dbl_generic(F, X, Y, Z):
+    a = F.sqr(X, "A")
+    b = F.sqr(Y, "B")
+    t = F.norm(F.shl(b, 3))
+    c8 = F.mul(t, b, "8C")
+    t = F.norm(F.shl(X, 2))
+    d = F.mul(t, b, "D")
+    e = F.norm(F.mul3(a))
+    t = F.norm(F.shl(Y, 1))
+    z3 = F.mul(t, Z, "Z3")
+    a = F.sqr(e, "F")
+    t = F.shl(d, 1)
+    x3 = F.norm(F.subk(a, t, "KB_64_29", "X3"))
+    t = F.mul3(d)
+    t = F.norm(F.subk(t, a, "KB_16_28", "3D-F"))
+    t = F.mul(e, t, "E(D-X3)")
+    y3 = F.norm(F.subk(t, c8, "KB_32_28", "Y3"))
+    return x3, y3, z3
+
+
+def jac_dbl(F, X, Y, Z):
+    return jac_dbl_generic(F, X, Y, Z) if F.two else jac_dbl_fp(X, Y, Z)
+
+
+def jac_madd(F, X, Y, Z, x2, y2):
+    z1z1 = F.sqr(Z, "Z1Z1")
+    h = F.mul(x2, z1z1, "U2")
+    h = F.norm(F.subk(h, X, "KB_128_31", "H"))
+    t = F.mul(y2, Z, "y2Z")
+    t = F.mul(t, z1z1, "S2")
+    r = F.norm(F.subk(t, Y, "KB_64_31", "r'"))
+    F.canon_ok(Z), F.canon_ok(h), F.canon_ok(r)
+    xd, yd, zd = jac_dbl(F, X, Y, Z)  # the equal-point branch
+    hh = F.sqr(h, "HH")
+    t = F.norm(F.shl(Z, 1))
+    z3 = F.mul(t, h, "Z3")
+    hh = F.norm(F.shl(hh, 2))
+    j = F.mul(h, hh, "J")
+    hh = F.mul(X, hh, "V")
+    t = F.sqr(r, "r'^2")
+    t = F.shl(t, 2)
+    t = F.subk(t, j, "KB_32_28", "X3a")
+    h2 = F.shl(hh, 1)
+    t = F.norm(F.subk(t, h2, "KB_64_29", "X3"))
+    hh = F.norm(F.subk(hh, t, "KB_128_28", "V-X3"))
+    r = F.norm(F.shl(r, 1))
+    hh = F.mul(r, hh, "r(V-X3)")
+    h = F.norm(F.shl(Y, 1))
+    j = F.mul(h, j, "2Y1J")
+    y3 = F.norm(F.subk(hh, j, "KB_32_28", "Y3"))
+    one = F.one()
+    jn = (lambda a, b: V2(vmax(a.c0, b.c0), vmax(a.c1, b.c1))) if F.two else vmax
+    return jn(jn(t, xd), x2), jn(jn(y3, yd), y2), jn(jn(z3, zd), one)
+
+
+def jac_add(F, X1, Y1, Z1, X2, Y2, Z2):
+    F.canon_ok(Z1), F.canon_ok(Z2)
+    z1z1 = F.sqr(Z1, "Z1Z1")
+    z2z2 = F.sqr(Z2, "Z2Z2")
+    u1 = F.mul(X1, z2z2, "U1")
+    s1 = F.mul(Y1, Z2, "Y1Z2")
+    s1 = F.mul(s1, z2z2, "S1")
+    h = F.mul(X2, z1z1, "U2")
+    h = F.norm(F.subk(h, u1, "KB_8_28", "H"))
+    r = F.mul(Y2, Z1, "Y2Z1")
+    r = F.mul(r, z1z1, "S2")
+    r = F.norm(F.subk(r, s1, "KB_8_28", "r'"))
+    F.canon_ok(h), F.canon_ok(r)
+    xd, yd, zd = jac_dbl(F, X1, Y1, Z1)
+    z1z1 = F.norm(F.shl(Z1, 1))
+    z1z1 = F.mul(z1z1, Z2, "2Z1Z2")
+    z3 = F.mul(z1z1, h, "Z3")
+    z1z1 = F.norm(F.shl(h, 1))
+    z1z1 = F.sqr(z1z1, "I")
+    z2z2 = F.mul(h, z1z1, "J")
+    u1 = F.mul(u1, z1z1, "V")
+    h = F.sqr(r, "r'^2")
+    h = F.shl(h, 2)
+    h = F.subk(h, z2z2, "KB_8_28", "X3a")
+    z1z1 = F.shl(u1, 1)
+    h = F.norm(F.subk(h, z1z1, "KB_64_29", "X3"))
+    u1 = F.norm(F.subk(u1, h, "KB_128_28", "V-X3"))
+    r = F.norm(F.shl(r, 1))
+    u1 = F.mul(r, u1, "r(V-X3)")
+    s1 = F.norm(F.shl(s1, 1))
+    s1 = F.mul(s1, z2z2, "2S1J")
+    y3 = F.norm(F.subk(u1, s1, "KB_8_28", "Y3"))
+    jn = (lambda a, b: V2(vmax(a.c0, b.c0), vmax(a.c1, b.c1))) if F.two else vmax
+    return jn(jn(h, xd), X2), jn(jn(y3, yd), Y2), jn(jn(z3, zd), Z2)
+
+
+def jac_eq_affine(F, X, Y, Z, x, y):
+    z2 = F.sqr(Z, "z2")
+    t = F.mul(x, z2, "xZ2")
+    t = F.subk(t, X, "KB_128_31", "eqx")
+    F.canon_ok(t)
+    z2 = F.mul(z2, Z, "z3")
+    t = F.mul(y, z2, "yZ3")
+    t = F.subk(t, Y, "KB_128_31", "eqy")
+    F.canon_ok(t)
+    F.canon_ok(Z)
+
+
+def join(F, a, b):
+    if F.two:
+        return V2(vmax(a.c0, b.c0), vmax(a.c1, b.c1))
+    return vmax(a, b)
+
+
+def _inflate1(a, f):
+    limbs = list(a.limbs)
+    limbs[NL - 1] = int(limbs[NL - 1] * f) + 2  # the top limb tracks the value
+    return V(limbs, a.val * f + 0.01)
+
+
+def _inflate(F, a, f=1.01):
+    if F.two:  # every Fp2 op returns exactly reduced(): the joined bound is already a fixed point
+        return a
+    return _inflate1(a, f)
+
+
+def _within(F, a, b):
+    """a subset of b (all bounds of a <= those of b)."""
+    pairs = ((a.c0, b.c0), (a.c1, b.c1)) if F.two else ((a, b),)
+    return all(all(x <= y for x, y in zip(u.limbs, w.limbs)) and u.val <= w.val for u, w in pairs)
+
+
+def ladder_invariant(F, base_x, base_y, add_base=None, rounds=12):
+    """A bound set S for the ladder accumulator (X, Y, Z) that contains the starting point and is
+    CLOSED under one ladder step (dbl, then optionally madd(base) or add(add_base)) — hence bounds
+    every state reached by mul_abs_u_affine / mul_abs_u_jac / in_subgroup_ref for any input.
+    Found by joined iteration, then inflated and verified closed."""
+    if add_base is None:
+        X, Y, Z = base_x, base_y, F.one()
+    else:
+        X, Y, Z = add_base
+
+    def step(X, Y, Z):
+        x1, y1, z1 = jac_dbl(F, X, Y, Z)
+        outs = [(x1, y1, z1)]
+        if add_base is None:
+            outs.append(jac_madd(F, x1, y1, z1, base_x, base_y))
+        else:
+            outs.append(jac_add(F, x1, y1, z1, *add_base))
+        nx, ny, nz = X, Y, Z
+        for ox, oy, oz in outs:
+            nx, ny, nz = join(F, nx, ox), join(F, ny, oy), join(F, nz, oz)
+        return nx, ny, nz
+
+    for _ in range(rounds):
+        X, Y, Z = step(X, Y, Z)
+    S = (_inflate(F, X), _inflate(F, Y), _inflate(F, Z))
+    for _ in range(40):
+        T = step(*S)
+        if all(_within(F, a, b) for a, b in zip(T, S)):
+            break
+        S = tuple(_inflate(F, join(F, a, b)) for a, b in zip(T, S))
+    else:
+        raise BoundError("ladder bound set is not closed: values keep growing")
+    return S

@@ -1,0 +1,120 @@
+"""Machine proof that the radix-2^28 arithmetic never overflows (CPU only).
+
+tests/field_bounds_model.py mirrors csrc/fp381.hpp + csrc/curve.hpp with exact interval bounds;
+every fp_mul column sum is checked < 2^64, every limb < 2^32, every borrowed constant dominates
+its subtrahend limb by limb, and the ladder states are shown to live in a bound set closed under
+the ladder steps (so the proof covers all 2^64 / 2^255 steps, every input point)."""
+from fractions import Fraction
+
+import pytest
+
+import field_bounds_model as M
+
+
+@pytest.mark.parametrize("two", [False, True], ids=["fp", "fp2"])
+def test_ladders_closed(two):
+    F = M.Field(two)
+    base = M.V2(M.normalized(Fraction(101, 100)), M.normalized(Fraction(101, 100))) if two else \
+        M.normalized(Fraction(101, 100))
+    S1 = M.ladder_invariant(F, base, base)                     # mul_abs_u_affine / in_subgroup_ref
+    if not two:
+        S2 = M.ladder_invariant(F, base, base, add_base=S1)    # mul_abs_u_jac (G1 second ladder)
+        beta_x = M.mul(base, M.normalized(1))
+        ny = M.norm(M.subk(M.normalized(0), base, "KB_64_31"))
+        M.jac_eq_affine(F, *S2, beta_x, ny)
+    M.jac_eq_affine(F, *S1, base, base)
+
+
+def _pow_pm3d4(a):
+    """fp_pow_pm3d4: table a, a^3, .., a^15 (via a^2), then squarings / table multiplies."""
+    a2 = M.mul(a, a, "a^2")
+    t = M.mul(a, a2, "tab")
+    for _ in range(8):
+        t = M.vmax(t, M.mul(t, a2, "tab"))
+    acc = t
+    for _ in range(460):
+        acc = M.vmax(M.mul(acc, acc, "sq"), M.mul(acc, t, "mul"))
+    return acc
+
+
+def test_sqrt_chain_inputs():
+    # G1 decompress: x < 2^381 < 1.24 p (range check happens in parallel), a = x^3 + 4
+    x = M.normalized(Fraction(124, 100))
+    xm = M.mul(x, M.normalized(1), "to_mont")
+    a = M.add_nr(M.mul(M.mul(xm, xm), xm), M.normalized(1))
+    t = _pow_pm3d4(a)
+    y = M.mul(t, a, "y")
+    M.canon_ok(M.subk(M.mul(y, y), a, "KB_64_31"), "fp_eq")
+    M.canon_ok(M.mul(y, M.normalized(Fraction(1, 10**6))), "from_mont")
+
+
+def _fp2_mont(v):
+    return M.mul(M.normalized(v), M.normalized(1), "to_mont")
+
+
+def test_fp2_sqrt_and_psi():
+    # G2 decompress (codec_kernels.hip k_g2_decompress / fp2_sqrt): everything reduced
+    xm = M.V2(_fp2_mont(Fraction(124, 100)), _fp2_mont(Fraction(124, 100)))
+    four = M.normalized(Fraction(1))
+    a = M.f2_mul(M.f2_sqr(xm), xm)
+    a = M.V2(M.add_red(a.c0, four), M.add_red(a.c1, four))
+    nrm = M.add_nr(M.mul(a.c0, a.c0), M.mul(a.c1, a.c1))
+    gam = M.mul(_pow_pm3d4(nrm), nrm, "gam")
+    M.canon_ok(M.subk(M.mul(gam, gam), nrm, "KB_64_31"), "gam^2 == N")
+    inv2 = M.normalized(1)
+    d = M.mul(M.add_nr(a.c0, gam), inv2, "d")
+    d = M.vmax(d, a.c0)
+    t = _pow_pm3d4(d)
+    s = M.mul(t, d, "s")
+    M.canon_ok(M.subk(M.mul(s, s), d, "KB_64_31"), "s^2 == d")
+    h = M.mul(M.mul(a.c1, t), inv2, "h")
+    nh = M.sub_red(M.normalized(0), h, "-h")
+    y = M.V2(M.vmax(s, nh), M.vmax(h, s))
+    y2 = M.f2_sqr(y)
+    M.canon_ok(M.sub_red(y2.c0, a.c0), "y^2 == a")
+    for c in (y.c0, y.c1):
+        M.canon_ok(M.mul(c, M.normalized(Fraction(1, 10**6))), "from_mont")
+    # G2 check kernel: on-curve test and psi(P) with canonical (range-checked) inputs
+    pm = M.V2(_fp2_mont(1), _fp2_mont(1))
+    lhs = M.f2_sqr(pm)
+    rhs = M.f2_mul(M.f2_sqr(pm), pm)
+    rhs = M.V2(M.add_red(rhs.c0, four), M.add_red(rhs.c1, four))
+    M.canon_ok(M.sub_red(lhs.c0, rhs.c0), "on-curve")
+    cx1 = M.normalized(1)
+    px = M.V2(M.mul(pm.c1, cx1), M.mul(pm.c0, cx1))
+    py = M.V2(pm.c0, M.sub_red(M.normalized(0), pm.c1))
+    py = M.f2_mul(py, M.V2(M.normalized(1), M.normalized(1)))
+    py = M.V2(M.sub_red(M.normalized(0), py.c0), M.sub_red(M.normalized(0), py.c1))
+    F = M.Field(True)
+    S1 = M.ladder_invariant(F, pm, pm)
+    M.jac_eq_affine(F, *S1, px, py)
+
+
+def test_bounds_model_catches_overflow():
+    wide = M.V([(1 << 31) - 1] * M.NL, 100)
+    with pytest.raises(M.BoundError):
+        M.mul(wide, wide)
+    with pytest.raises(M.BoundError):
+        M.subk(M.normalized(1), wide, "KB_2_28")
+
+
+def test_synth_madd_chain():
+    """k_synth (synth_kernels.hip): 31 back-to-back mixed additions of table points (no doubling
+    in between), then to_affine. Bound set closed under madd alone."""
+    F = M.Field(False)
+    base = M.normalized(Fraction(101, 100))
+    S = (base, base, M.normalized(1))
+    for _ in range(40):
+        T = M.jac_madd(F, *S, base, base)
+        T = tuple(M.join(F, a, b) for a, b in zip(S, T))
+        if all(M._within(F, a, b) for a, b in zip(T, S)):
+            break
+        S = tuple(M._inflate(F, t) for t in T)
+    else:
+        raise AssertionError("madd chain bound set not closed")
+    X, Y, Z = S
+    zi = _pow_pm3d4(Z)
+    zi = M.mul(M.mul(M.mul(zi, zi), zi), Z, "inv")
+    z2 = M.mul(zi, zi)
+    M.canon_ok(M.mul(X, z2), "x")
+    M.canon_ok(M.mul(Y, M.mul(z2, zi)), "y")
