@@ -61,8 +61,8 @@ KZG_DEV void jac_dbl(jac<fp>& p) {
   fp a, b, c8, d, e, t;
   fp_sqr(a, p.x);              // A = X^2                    N
   fp_sqr(b, p.y);              // B = Y^2                    N
-  fp_shl_nr<3>(t, b);          // 8B                        < 2^31
-  fp_mul(c8, t, b);            // 8C = 8 B^2                 N
+  fp_shl_nr<1>(t, b);          // 2B                        < 2^29
+  fp_sqr(c8, t);               // 4C = (2B)^2                N
   fp_shl_nr<2>(t, p.x);        // 4X                        < 2^32
   fp_mul(d, t, b);             // D = 4 X B                  N
   fp_mul3_nr(e, a);            // E = 3A                    < 3 * 2^28
@@ -74,7 +74,8 @@ KZG_DEV void jac_dbl(jac<fp>& p) {
   fp_mul3_nr(t, d);            // 3D
   fp_subk_nr(t, t, a, KB_8_28);    // D - X3 = 3D - F       < 5 * 2^28
   fp_mul(t, e, t);             // E (D - X3)                 N
-  fp_subk_nr(p.y, t, c8, KB_8_28); // Y3 = E (D - X3) - 8C  < 2^30
+  fp_shl_nr<1>(c8, c8);        // 8C                        < 2^29
+  fp_subk_nr(p.y, t, c8, KB_8_29); // Y3 = E (D - X3) - 8C  < 2^30
 }
 
 // Generic (Fp2, cold): all values reduced (< 2p) through the Fp2 helpers above.

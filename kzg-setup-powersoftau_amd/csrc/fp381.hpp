@@ -75,7 +75,37 @@ KZG_DEV void fp_mul(fp& r, const fp& a, const fp& b) {
     acc >>= 28;
   }
 }
-KZG_DEV void fp_sqr(fp& r, const fp& a) { fp_mul(r, a, a); }
+// r = a^2 R^-1 mod p: each cross product a_j a_k (j < k) once, as a_j (2 a_k), plus the squares —
+// 105 instead of 196 products for the a*a half (the 196 m*p products of the reduction stay).
+// Every column partial sum is at most fp_mul(a, a)'s, so the same bounds hold; in addition
+// a's limbs must be < 2^31 so that 2 a_k fits 32 bits.
+KZG_DEV void fp_sqr(fp& r, const fp& a) {
+  uint32_t d[NL], m[NL];
+#pragma unroll
+  for (int j = 0; j < NL; j++) d[j] = a.v[j] << 1;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < 2 * NL - 1; i++) {
+    const int j0 = i < NL ? 0 : i - (NL - 1);
+    uint64_t accp = 0;
+#pragma unroll
+    for (int j = j0; 2 * j < i; j++) acc += (uint64_t)a.v[j] * d[i - j];
+    if ((i & 1) == 0) acc += (uint64_t)a.v[i / 2] * a.v[i / 2];
+    const int k0 = i < NL ? 0 : i - (NL - 1);
+    const int k1 = i < NL ? i - 1 : NL - 1;
+#pragma unroll
+    for (int k = k0; k <= k1; k++) accp += (uint64_t)m[k] * FP_P[i - k];
+    acc += accp;
+    if (i < NL) {
+      m[i] = ((uint32_t)acc * FP_PINV) & LMASK;
+      acc += (uint64_t)m[i] * FP_P[0];
+    } else {
+      r.v[i - NL] = (uint32_t)acc & LMASK;
+    }
+    acc >>= 28;
+  }
+  r.v[NL - 1] = (uint32_t)acc & LMASK;  // column 2 NL - 1 holds only the carry
+}
 
 // ------------------------------------------------------------------------------- limb-wise ops
 KZG_DEV void fp_add_nr(fp& r, const fp& a, const fp& b) {
@@ -321,7 +351,7 @@ struct fp2 {
 };
 // Fp versions of the generic field interface used by curve.hpp
 KZG_DEV void f_mul(fp& r, const fp& a, const fp& b) { fp_mul(r, a, b); }
-KZG_DEV void f_sqr(fp& r, const fp& a) { fp_mul(r, a, a); }
+KZG_DEV void f_sqr(fp& r, const fp& a) { fp_sqr(r, a); }
 KZG_DEV bool f_is_zero(const fp& a) { return fp_is_zero(a); }
 KZG_DEV void f_one(fp& r) { fp_set(r, FP_ONE); }
 KZG_DEV void f_norm(fp& r, const fp& a) { fp_norm(r, a); }

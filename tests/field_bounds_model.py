@@ -93,6 +93,13 @@ def mul(a: V, b: V, name="mul"):
     return out
 
 
+def sqr(a: V, name="sqr"):
+    """fp_sqr: same column sums as mul(a, a); the doubled operand 2 a_k must fit 32 bits."""
+    if max(a.limbs) >= 1 << 31:
+        raise BoundError(f"{name}: squaring input limb >= 2^31 ({a!r})")
+    return mul(a, a, name)
+
+
 def add_nr(a, b, name="add"):
     return V([x + y for x, y in zip(a.limbs, b.limbs)], (a.val + b.val) * UP, name)
 
@@ -198,7 +205,7 @@ class Field:
         return f2_mul(a, b, name) if self.two else mul(a, b, name)
 
     def sqr(self, a, name="sqr"):
-        return f2_sqr(a, name) if self.two else mul(a, a, name)
+        return f2_sqr(a, name) if self.two else sqr(a, name)
 
     def subk(self, a, b, k, name="subk"):
         if self.two:
@@ -236,22 +243,23 @@ class Field:
 # formulas (mirror csrc/curve.hpp)
 def jac_dbl_fp(X, Y, Z):
     """jac_dbl(jac<fp>&) — the hot path."""
-    a = mul(X, X, "A")
-    b = mul(Y, Y, "B")
-    t = shl(b, 3)
-    c8 = mul(t, b, "8C")
+    a = sqr(X, "A")
+    b = sqr(Y, "B")
+    t = shl(b, 1)
+    c4 = sqr(t, "4C")
     t = shl(X, 2)
     d = mul(t, b, "D")
     e = mul3(a)
     t = shl(Y, 1)
     z3 = mul(t, Z, "Z3")
-    a = mul(e, e, "F")
+    a = sqr(e, "F")
     t = shl(d, 1)
     x3 = subk(a, t, "KB_8_29", "X3")
     t = mul3(d)
     t = subk(t, a, "KB_8_28", "3D-F")
     t = mul(e, t, "E(D-X3)")
-    y3 = subk(t, c8, "KB_8_28", "Y3")
+    c8 = shl(c4, 1)
+    y3 = subk(t, c8, "KB_8_29", "Y3")
     return x3, y3, z3
 
 

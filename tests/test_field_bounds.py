@@ -27,13 +27,13 @@ def test_ladders_closed(two):
 
 def _pow_pm3d4(a):
     """fp_pow_pm3d4: table a, a^3, .., a^15 (via a^2), then squarings / table multiplies."""
-    a2 = M.mul(a, a, "a^2")
+    a2 = M.sqr(a, "a^2")
     t = M.mul(a, a2, "tab")
     for _ in range(8):
         t = M.vmax(t, M.mul(t, a2, "tab"))
     acc = t
     for _ in range(460):
-        acc = M.vmax(M.mul(acc, acc, "sq"), M.mul(acc, t, "mul"))
+        acc = M.vmax(M.sqr(acc, "sq"), M.mul(acc, t, "mul"))
     return acc
 
 

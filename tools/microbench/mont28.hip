@@ -52,6 +52,34 @@ __device__ __forceinline__ void mont28(uint32_t r[14], const uint32_t a[14], con
   }
 }
 
+// dedicated squaring: cross products once (a_j * 2 a_k), then the same interleaved REDC
+__device__ __forceinline__ void sqr28(uint32_t r[14], const uint32_t a[14]) {
+  uint32_t d[14], m[14];
+#pragma unroll
+  for (int j = 0; j < 14; j++) d[j] = a[j] << 1;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < 27; i++) {
+    const int j0 = i < 14 ? 0 : i - 13;
+    uint64_t accp = 0;
+#pragma unroll
+    for (int j = j0; 2 * j < i; j++) acc += (uint64_t)a[j] * d[i - j];
+    if ((i & 1) == 0) acc += (uint64_t)a[i / 2] * a[i / 2];
+    const int k1 = i < 14 ? i - 1 : 13;
+#pragma unroll
+    for (int k = j0; k <= k1; k++) accp += (uint64_t)m[k] * P28[i - k];
+    acc += accp;
+    if (i < 14) {
+      m[i] = ((uint32_t)acc * PINV28) & M28;
+      acc += (uint64_t)m[i] * P28[0];
+    } else {
+      r[i - 14] = (uint32_t)acc & M28;
+    }
+    acc >>= 28;
+  }
+  r[13] = (uint32_t)acc & M28;
+}
+
 template <int V, int CH>
 __global__ void __launch_bounds__(256) kmont(uint32_t* out, const uint32_t* in, int iters, int lds_pad) {
   extern __shared__ uint32_t pad[];
@@ -65,7 +93,10 @@ __global__ void __launch_bounds__(256) kmont(uint32_t* out, const uint32_t* in, 
   }
   for (int it = 0; it < iters; it++) {
 #pragma unroll
-    for (int c = 0; c < CH; c++) mont28<V>(x[c], x[c], y);
+    for (int c = 0; c < CH; c++) {
+      if (V == 2) sqr28(x[c], x[c]);
+      else mont28<V>(x[c], x[c], y);
+    }
   }
   uint32_t s = 0;
 #pragma unroll
@@ -81,7 +112,8 @@ __global__ void kcheck(uint32_t* out, const uint32_t* in) {
   int t = threadIdx.x;
   uint32_t a[14], b[14], r[14];
   for (int j = 0; j < 14; j++) a[j] = in[t * 28 + j], b[j] = in[t * 28 + 14 + j];
-  mont28<V>(r, a, b);
+  if (V == 2) sqr28(r, a);
+  else mont28<V>(r, a, b);
   for (int j = 0; j < 14; j++) out[t * 14 + j] = r[j];
 }
 
@@ -128,12 +160,23 @@ int main() {
     }
     printf("check V=%d: %d/64 mismatches\n", v, bad);
   }
+  {
+    uint32_t hout[64 * 14], ref[14];
+    hipLaunchKernelGGL(kcheck<2>, 1, 64, 0, 0, out, in);
+    CHECK(hipMemcpy(hout, out, sizeof hout, hipMemcpyDeviceToHost));
+    int bad = 0;
+    for (int t = 0; t < 64; t++) {
+      mont_ref(ref, cin + t * 28, cin + t * 28);
+      for (int j = 0; j < 14; j++) if (ref[j] != hout[t * 14 + j]) { bad++; break; }
+    }
+    printf("check sqr: %d/64 mismatches\n", bad);
+  }
   CHECK(hipMemcpy(in, hin, 4096 * 4, hipMemcpyHostToDevice));
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
   const int occ[4] = {1, 2, 4, 8};
-  for (int v = 0; v < 3; v++)
+  for (int v = 0; v < 5; v++)
     for (int oi = 0; oi < 4; oi++) {
       size_t lds = (160 * 1024) / occ[oi] - 1024;
       int iters = 100;
@@ -143,11 +186,13 @@ int main() {
         if (v == 0) hipLaunchKernelGGL((kmont<0, 1>), blocks, threads, lds, 0, out, in, iters, 0);
         if (v == 1) hipLaunchKernelGGL((kmont<1, 1>), blocks, threads, lds, 0, out, in, iters, 0);
         if (v == 2) hipLaunchKernelGGL((kmont<0, 2>), blocks, threads, lds, 0, out, in, iters / 2, 0);
+        if (v == 3) hipLaunchKernelGGL((kmont<2, 1>), blocks, threads, lds, 0, out, in, iters, 0);
+        if (v == 4) hipLaunchKernelGGL((kmont<2, 2>), blocks, threads, lds, 0, out, in, iters / 2, 0);
         CHECK(hipEventRecord(e1));
         CHECK(hipEventSynchronize(e1));
         CHECK(hipEventElapsedTime(&ms, e0, e1));
       }
-      const char* nm[3] = {"R28 single acc", "R28 two acc", "R28 2 chains"};
+      const char* nm[5] = {"R28 single acc", "R28 two acc", "R28 2 chains", "R28 sqr", "R28 sqr 2 chains"};
       printf("%-16s waves/SIMD<=%d: %8.3f ms  %7.2f G fp-mul/s\n", nm[v], occ[oi], ms,
              (double)blocks * threads * iters / ms / 1e6);
     }
