@@ -49,6 +49,7 @@ def parse():
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-log2", type=int, default=15)
+    ap.add_argument("--no-next-rows", action="store_true", help="skip the loader (SURVEY 8f) measurement")
     return ap.parse_args()
 
 
@@ -185,6 +186,28 @@ def main():
     else:
         bad = min(D.read_key(key1), D.read_key(key2))
 
+    # SURVEY §8f row 2 (loader mirror), measured after the timed region on rank 0: the G1 ark
+    # records just produced -> in-memory GroupAffine (deserialize_unchecked), HBM-bound.
+    next_rows = None
+    if rank == 0 and not args.no_next_rows:
+        outl = torch.empty(m1 * 104, dtype=torch.uint8, device=dev)
+        keyl = torch.empty(1, dtype=torch.int64, device=dev)
+        D.codec_dev("g1_load", out1, outl, keyl)
+        le = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        le[0].record()
+        for _ in range(5):
+            D.codec_dev("g1_load", out1, outl, keyl)
+        le[1].record()
+        torch.cuda.synchronize()
+        load_ms = le[0].elapsed_time(le[1]) / 5
+        load_gbs = 200 * m1 / (load_ms * 1e-3) / 1e9
+        next_rows = {"g1_deserialize_unchecked": {
+            "kernel": "k_g1_load (load_kzg_setup per-point work)", "points": m1, "launch_ms": load_ms,
+            "points_per_s": m1 / (load_ms * 1e-3), "algorithmic_bytes_per_point": 200,
+            "achieved_GBs": load_gbs, "peak_GBs": HBM_PEAK_GBS, "hbm_frac": load_gbs / HBM_PEAK_GBS,
+            "all_accepted": D.read_key(keyl) == KD.NO_BAD}}
+        del outl
+
     g1_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / len(ev)
     g2_ms = sum(e[1].elapsed_time(e[2]) for e in ev) / len(ev)
     ms_per_step = elapsed * 1e3 / args.steps
@@ -237,6 +260,8 @@ def main():
             "rejected_points": 0 if bad == KD.NO_BAD else 1,
             "generate_s": t_gen,
         }
+        if next_rows:
+            result["next_rows"] = next_rows
         if world == 1 and not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(comp1, comp2, args.cpu_sample_log2)
         print(json.dumps(result), flush=True)

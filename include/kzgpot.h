@@ -111,6 +111,45 @@ int kzgpot_preprocess(const char* transcript_path, const char* out_path, int mod
 int kzgpot_preprocess_buffer(const uint8_t* transcript, size_t len, uint8_t* out, int mode, uint32_t n_log2,
                              int n_gpus, int* bad_section, int64_t* bad_index);
 
+/* ---------------------------------------------------------------- loader mirror (next-row §8f 2) */
+/* ark-ec 0.2 GroupAffine in memory (what `deserialize_unchecked` returns): each Fp as 6 LE u64 in
+ * ark-ff Montgomery form (R = 2^384), then `infinity` (u8) and zero padding to 8 B:
+ *   G1 104 B = x[48] y[48] inf[1] pad[7];  G2 200 B = x.c0 x.c1 y.c0 y.c1 [4 x 48] inf[1] pad[7].
+ * A Rust caller reads these as #[repr(C)] mirrors of GroupAffine. */
+#define KZGPOT_G1_ARK_MONT_BYTES 104
+#define KZGPOT_G2_ARK_MONT_BYTES 200
+/* ark-uncompressed G1 (96 B) → GroupAffine (104 B): ArkG1Affine::deserialize_unchecked (src/lib.rs:180,
+ * 183) — coordinates < p and SWFlags checked, NO curve and NO subgroup check. */
+int kzgpot_g1_deserialize_unchecked(const uint8_t* in, size_t n, uint8_t* out, int64_t* first_bad);
+/* ark-uncompressed G2 (192 B) → GroupAffine (200 B): ArkG2Affine::deserialize_unchecked (src/lib.rs:209-215). */
+int kzgpot_g2_deserialize_unchecked(const uint8_t* in, size_t n, uint8_t* out, int64_t* first_bad);
+int kzgpot_g1_deserialize_unchecked_ex(const uint8_t* in, size_t n, uint8_t* out, int64_t* first_bad, uint8_t* status);
+int kzgpot_g2_deserialize_unchecked_ex(const uint8_t* in, size_t n, uint8_t* out, int64_t* first_bad, uint8_t* status);
+int kzgpot_g1_deserialize_unchecked_dev(const void* d_in, size_t n, void* d_out, uint64_t* d_bad_key,
+                                        uint8_t* d_status, void* stream);
+int kzgpot_g2_deserialize_unchecked_dev(const void* d_in, size_t n, void* d_out, uint64_t* d_bad_key,
+                                        uint8_t* d_status, void* stream);
+/* load_kzg_setup (src/lib.rs:174-195) for 2^n_log2 powers (the reference fixes n_log2 = 21):
+ * powers_of_g (2N-1 G1), powers_of_gamma_g (N G1), vk = g, gamma_g (G1), h, beta_h (G2) =
+ * 2 x 104 + 2 x 200 B (VerifierKey::deserialize_unchecked; prepared_h / prepared_beta_h are the
+ * caller's `h.into()` / `beta_h.into()`). Output buffers in the layout above. Trailing bytes are
+ * ignored, as by the reference's sequential reader; a short file is KZGPOT_E_SIZE. On a rejected
+ * point *bad_section (0 powers_of_g, 1 powers_of_gamma_g, 2 vk/h-beta_h, 3 powers_of_h) and
+ * *bad_index locate it. */
+int kzgpot_load_kzg_setup(const char* path, uint32_t n_log2, uint8_t* powers_of_g, uint8_t* powers_of_gamma_g,
+                          uint8_t* vk, int* bad_section, int64_t* bad_index);
+int kzgpot_load_kzg_setup_buffer(const uint8_t* file, size_t len, uint32_t n_log2, uint8_t* powers_of_g,
+                                 uint8_t* powers_of_gamma_g, uint8_t* vk, int* bad_section, int64_t* bad_index);
+/* load_fastkzg_setup (src/lib.rs:197-228): powers_of_g, powers_of_gamma_g, h_beta_h = h, beta_h
+ * (2 x 200 B, as read: prepared_beta_h = beta_h.into()), powers_of_h (N G2). UniversalParams.beta_h
+ * is powers_of_h[1] in the reference (src/lib.rs:221), not the beta_h read from the file. NB: the
+ * reference opens KZG_SETUP_FILE here (src/lib.rs:198); this entry point takes the path. */
+int kzgpot_load_fastkzg_setup(const char* path, uint32_t n_log2, uint8_t* powers_of_g, uint8_t* powers_of_gamma_g,
+                              uint8_t* h_beta_h, uint8_t* powers_of_h, int* bad_section, int64_t* bad_index);
+int kzgpot_load_fastkzg_setup_buffer(const uint8_t* file, size_t len, uint32_t n_log2, uint8_t* powers_of_g,
+                                     uint8_t* powers_of_gamma_g, uint8_t* h_beta_h, uint8_t* powers_of_h,
+                                     int* bad_section, int64_t* bad_index);
+
 /* ---------------------------------------------------------------- misc */
 const char* kzgpot_status_name(int status);  /* name of a KZGPOT_ST_* or KZGPOT_E_* code */
 int kzgpot_device_count(void);               /* visible HIP devices (0 if none) */

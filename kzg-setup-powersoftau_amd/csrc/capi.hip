@@ -274,6 +274,130 @@ int kzgpot_preprocess(const char* transcript_path, const char* out_path, int mod
   return (put == out.size() && cr == 0) ? 0 : KZGPOT_E_IO;
 }
 
+// ------------------------------------------------------------------------------- loader mirror
+int kzgpot_g1_deserialize_unchecked_ex(const uint8_t* in, size_t n, uint8_t* out, int64_t* first_bad,
+                                       uint8_t* status) {
+  return run_host(current_device(), CodecOp::G1Load, in, n, out, 0, first_bad, status);
+}
+int kzgpot_g2_deserialize_unchecked_ex(const uint8_t* in, size_t n, uint8_t* out, int64_t* first_bad,
+                                       uint8_t* status) {
+  return run_host(current_device(), CodecOp::G2Load, in, n, out, 0, first_bad, status);
+}
+int kzgpot_g1_deserialize_unchecked(const uint8_t* in, size_t n, uint8_t* out, int64_t* first_bad) {
+  return kzgpot_g1_deserialize_unchecked_ex(in, n, out, first_bad, nullptr);
+}
+int kzgpot_g2_deserialize_unchecked(const uint8_t* in, size_t n, uint8_t* out, int64_t* first_bad) {
+  return kzgpot_g2_deserialize_unchecked_ex(in, n, out, first_bad, nullptr);
+}
+int kzgpot_g1_deserialize_unchecked_dev(const void* d_in, size_t n, void* d_out, uint64_t* d_bad_key,
+                                        uint8_t* d_status, void* stream) {
+  return run_dev(CodecOp::G1Load, d_in, n, d_out, 0, d_bad_key, d_status, stream);
+}
+int kzgpot_g2_deserialize_unchecked_dev(const void* d_in, size_t n, void* d_out, uint64_t* d_bad_key,
+                                        uint8_t* d_status, void* stream) {
+  return run_dev(CodecOp::G2Load, d_in, n, d_out, 0, d_bad_key, d_status, stream);
+}
+
+}  // extern "C"
+
+namespace {
+// One sequential pass over a setup file: each section is `count` ark-uncompressed points read
+// with deserialize_unchecked into `dst`. Mirrors the reference's BufReader loop (no size check
+// beyond "enough bytes").
+struct LoadSection {
+  CodecOp op;
+  uint64_t count;
+  uint8_t* dst;
+  int section;  // reported in *bad_section
+};
+int load_sections(const uint8_t* file, size_t len, const LoadSection* secs, int nsec, int* bad_section,
+                  int64_t* bad_index) {
+  if (bad_section) *bad_section = -1;
+  if (bad_index) *bad_index = -1;
+  if (!file) return KZGPOT_E_INVALID_ARG;
+  uint64_t need = 0;
+  for (int k = 0; k < nsec; k++) {
+    if (!secs[k].dst) return KZGPOT_E_INVALID_ARG;
+    need += secs[k].count * in_record(secs[k].op);
+  }
+  if (len < need) return KZGPOT_E_SIZE;
+  if (device_count() <= 0) return KZGPOT_E_DEVICE;
+  const uint8_t* p = file;
+  for (int k = 0; k < nsec; k++) {
+    int64_t fb = -1;
+    const int r = run_host(current_device(), secs[k].op, p, secs[k].count, secs[k].dst, 0, &fb, nullptr);
+    if (r) {
+      if (bad_section) *bad_section = secs[k].section;
+      if (bad_index) *bad_index = fb;
+      return r;
+    }
+    p += secs[k].count * in_record(secs[k].op);
+  }
+  return 0;
+}
+int read_file(const char* path, std::vector<uint8_t>& buf) {
+  if (!path) return KZGPOT_E_INVALID_ARG;
+  FILE* f = fopen(path, "rb");
+  if (!f) return KZGPOT_E_IO;
+  fseek(f, 0, SEEK_END);
+  const long len = ftell(f);
+  fseek(f, 0, SEEK_SET);
+  if (len < 0) {
+    fclose(f);
+    return KZGPOT_E_IO;
+  }
+  buf.resize((size_t)len);
+  const size_t got = fread(buf.data(), 1, buf.size(), f);
+  fclose(f);
+  return got == buf.size() ? 0 : KZGPOT_E_IO;
+}
+}  // namespace
+
+extern "C" {
+
+int kzgpot_load_kzg_setup_buffer(const uint8_t* file, size_t len, uint32_t n_log2, uint8_t* powers_of_g,
+                                 uint8_t* powers_of_gamma_g, uint8_t* vk, int* bad_section, int64_t* bad_index) {
+  if (n_log2 > 30 || !vk) return KZGPOT_E_INVALID_ARG;
+  const uint64_t n = 1ull << n_log2;
+  const uint64_t g1 = KZGPOT_G1_ARK_MONT_BYTES;
+  const LoadSection secs[] = {
+      {CodecOp::G1Load, 2 * n - 1, powers_of_g, 0},      // TAU_POWERS_G1_LENGTH (src/lib.rs:179-181)
+      {CodecOp::G1Load, n, powers_of_gamma_g, 1},        // TAU_POWERS_LENGTH (src/lib.rs:182-184)
+      {CodecOp::G1Load, 2, vk, 2},                       // VerifierKey g, gamma_g
+      {CodecOp::G2Load, 2, vk + 2 * g1, 2},              // VerifierKey h, beta_h
+  };
+  return load_sections(file, len, secs, 4, bad_section, bad_index);
+}
+int kzgpot_load_kzg_setup(const char* path, uint32_t n_log2, uint8_t* powers_of_g, uint8_t* powers_of_gamma_g,
+                          uint8_t* vk, int* bad_section, int64_t* bad_index) {
+  std::vector<uint8_t> buf;
+  const int r = read_file(path, buf);
+  if (r) return r;
+  return kzgpot_load_kzg_setup_buffer(buf.data(), buf.size(), n_log2, powers_of_g, powers_of_gamma_g, vk,
+                                      bad_section, bad_index);
+}
+int kzgpot_load_fastkzg_setup_buffer(const uint8_t* file, size_t len, uint32_t n_log2, uint8_t* powers_of_g,
+                                     uint8_t* powers_of_gamma_g, uint8_t* h_beta_h, uint8_t* powers_of_h,
+                                     int* bad_section, int64_t* bad_index) {
+  if (n_log2 > 30) return KZGPOT_E_INVALID_ARG;
+  const uint64_t n = 1ull << n_log2;
+  const LoadSection secs[] = {
+      {CodecOp::G1Load, 2 * n - 1, powers_of_g, 0},  // src/lib.rs:204-206
+      {CodecOp::G1Load, n, powers_of_gamma_g, 1},    // src/lib.rs:207-209 (BTreeMap keys 0..N-1)
+      {CodecOp::G2Load, 2, h_beta_h, 2},             // h, beta_h (src/lib.rs:211-212)
+      {CodecOp::G2Load, n, powers_of_h, 3},          // src/lib.rs:214-217
+  };
+  return load_sections(file, len, secs, 4, bad_section, bad_index);
+}
+int kzgpot_load_fastkzg_setup(const char* path, uint32_t n_log2, uint8_t* powers_of_g, uint8_t* powers_of_gamma_g,
+                              uint8_t* h_beta_h, uint8_t* powers_of_h, int* bad_section, int64_t* bad_index) {
+  std::vector<uint8_t> buf;
+  const int r = read_file(path, buf);
+  if (r) return r;
+  return kzgpot_load_fastkzg_setup_buffer(buf.data(), buf.size(), n_log2, powers_of_g, powers_of_gamma_g,
+                                          h_beta_h, powers_of_h, bad_section, bad_index);
+}
+
 const char* kzgpot_status_name(int s) {
   switch (s < 0 && s > -100 ? -s : s) {
     case KZGPOT_OK: return "ok";

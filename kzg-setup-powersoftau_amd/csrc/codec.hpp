@@ -9,15 +9,35 @@ namespace kzgpot {
 
 constexpr int kBlock = 256;  // 4 waves; one point per lane
 
-enum class CodecOp { G1Decompress, G2Decompress, G1Transcode, G2Transcode };
+enum class CodecOp { G1Decompress, G2Decompress, G1Transcode, G2Transcode, G1Load, G2Load };
 
 // record sizes on the wire
 constexpr uint64_t in_record(CodecOp op) {
-  return op == CodecOp::G1Decompress ? 48 : op == CodecOp::G2Decompress ? 96 : op == CodecOp::G1Transcode ? 96 : 192;
+  switch (op) {
+    case CodecOp::G1Decompress: return 48;
+    case CodecOp::G2Decompress: return 96;
+    case CodecOp::G1Transcode: return 96;
+    case CodecOp::G2Transcode: return 192;
+    case CodecOp::G1Load: return 96;
+    case CodecOp::G2Load: return 192;
+  }
+  return 0;
 }
 constexpr uint64_t out_record(CodecOp op) {
-  return (op == CodecOp::G1Decompress || op == CodecOp::G1Transcode) ? 96 : 192;
+  switch (op) {
+    case CodecOp::G1Decompress: return 96;
+    case CodecOp::G2Decompress: return 192;
+    case CodecOp::G1Transcode: return 96;
+    case CodecOp::G2Transcode: return 192;
+    case CodecOp::G1Load: return KZGPOT_G1_ARK_MONT_BYTES;
+    case CodecOp::G2Load: return KZGPOT_G2_ARK_MONT_BYTES;
+  }
+  return 0;
 }
+
+// loader kernels (load_kernels.hip)
+hipError_t launch_load(bool g2, const void* d_in, void* d_out, uint64_t n, unsigned long long* d_first_bad,
+                       uint8_t* d_status, hipStream_t stream);
 
 hipError_t launch_codec(CodecOp op, const void* d_in, void* d_out, uint64_t n, uint32_t flags,
                         unsigned long long* d_first_bad, uint8_t* d_status, hipStream_t stream);

@@ -42,17 +42,18 @@ MODE_FASTKZG = 1
 ST_OK, ST_COMPRESSION_MODE, ST_UNEXPECTED_INFO, ST_NOT_IN_FIELD = 0, 1, 2, 3
 ST_NOT_ON_CURVE, ST_NOT_IN_SUBGROUP, ST_UNEXPECTED_FLAGS, ST_INFINITY = 4, 5, 6, 7
 SECTIONS = ("tau_g1", "tau_g2", "alpha_g1", "beta_g1", "beta_g2")
+LOAD_SECTIONS = ("powers_of_g", "powers_of_gamma_g", "vk / h, beta_h", "powers_of_h")
 
 
 class KzgPotError(RuntimeError):
-    def __init__(self, code: int, first_bad: int = -1, section: int = -1):
+    def __init__(self, code: int, first_bad: int = -1, section: int = -1, section_names=SECTIONS):
         self.code = code
         self.first_bad = first_bad
         self.section = section
         name = status_name(code)
         where = f" at index {first_bad}" if first_bad >= 0 else ""
         if section >= 0:
-            where += f" in section {SECTIONS[section]}"
+            where += f" in section {section_names[section]}"
         super().__init__(f"kzgpot error {code} ({name}){where}")
 
 
@@ -179,6 +180,119 @@ def preprocess_kgz(transcript_path: str = "powersoftau", out_path: str = KZG_SET
 
 def preprocess_fastkgz(transcript_path: str = "powersoftau", out_path: str = KZG_SETUP_FILE, **kw) -> None:
     preprocess(transcript_path, out_path, MODE_FASTKZG, **kw)
+
+
+# ------------------------------------------------------------------ loader mirror (src/lib.rs:174-228)
+G1_ARK_MONT_BYTES = 104  # in-memory GroupAffine<g1>: x, y as 6 LE u64 Montgomery (R = 2^384), infinity, pad
+G2_ARK_MONT_BYTES = 200
+
+
+def deserialize_unchecked(data, g2: bool = False, want_status: bool = False) -> CodecResult:
+    """ark-ec 0.2 `GroupAffine::deserialize_unchecked` over packed ark-uncompressed records
+    (96 B G1 / 192 B G2) → in-memory GroupAffine records (104 / 200 B). Coordinates < p and
+    SWFlags are checked; no curve or subgroup check (that is what "unchecked" means)."""
+    rin, rout = (192, G2_ARK_MONT_BYTES) if g2 else (96, G1_ARK_MONT_BYTES)
+    fname = "kzgpot_g2_deserialize_unchecked_ex" if g2 else "kzgpot_g1_deserialize_unchecked_ex"
+    ptr, nbytes, keep = _buf(data)
+    if nbytes % rin:
+        raise ValueError(f"deserialize_unchecked: input length {nbytes} is not a multiple of {rin}")
+    n = nbytes // rin
+    out = ctypes.create_string_buffer(max(1, n * rout))
+    st = ctypes.create_string_buffer(max(1, n)) if want_status else None
+    fb = ctypes.c_int64(-1)
+    ret = getattr(_lib.load(), fname)(ptr, n, out, ctypes.byref(fb), st)
+    del keep
+    if ret <= -100:
+        raise KzgPotError(ret)
+    return CodecResult(out.raw[: n * rout], ret, fb.value, st.raw[:n] if st is not None else None)
+
+
+def _records(buf, rec: int):
+    import numpy as np
+    return np.frombuffer(buf, dtype=np.uint8).reshape(-1, rec)
+
+
+@dataclass
+class Powers:
+    """ark-poly-commit 0.2 `kzg10::Powers` (Cow::Owned): rows are in-memory GroupAffine<g1>."""
+    powers_of_g: object        # (2N-1, 104) uint8
+    powers_of_gamma_g: object  # (N, 104) uint8
+
+
+@dataclass
+class VerifierKey:
+    """ark-poly-commit 0.2 `kzg10::VerifierKey`. prepared_h / prepared_beta_h are the pairing
+    precomputations `h.into()` / `beta_h.into()` the consumer builds from these two points."""
+    g: bytes
+    gamma_g: bytes
+    h: bytes
+    beta_h: bytes
+
+
+@dataclass
+class UniversalParams:
+    """ark-poly-commit 0.2 `kzg10::UniversalParams` as built by load_fastkzg_setup (src/lib.rs:219-227).
+    powers_of_gamma_g row i is the BTreeMap entry with key i. beta_h = powers_of_h[1] (lib.rs:221);
+    prepared_beta_h is built from `beta_h_read`, the point stored after h in the file."""
+    powers_of_g: object
+    powers_of_gamma_g: object
+    h: bytes
+    beta_h: bytes
+    beta_h_read: bytes
+
+
+def _load_err(r, sec, idx):
+    if r:
+        raise KzgPotError(r, idx.value, sec.value, LOAD_SECTIONS)
+
+
+def load_kzg_setup_buffer(data, n_log2: int = TAU_POWERS_LOG2):
+    n = 1 << n_log2
+    ptr, nbytes, keep = _buf(data)
+    pg = ctypes.create_string_buffer((2 * n - 1) * G1_ARK_MONT_BYTES)
+    pgg = ctypes.create_string_buffer(n * G1_ARK_MONT_BYTES)
+    vk = ctypes.create_string_buffer(2 * G1_ARK_MONT_BYTES + 2 * G2_ARK_MONT_BYTES)
+    sec, idx = ctypes.c_int(-1), ctypes.c_int64(-1)
+    r = _lib.load().kzgpot_load_kzg_setup_buffer(ptr, nbytes, n_log2, pg, pgg, vk, ctypes.byref(sec),
+                                                 ctypes.byref(idx))
+    del keep
+    _load_err(r, sec, idx)
+    v, a = vk.raw, G1_ARK_MONT_BYTES
+    return (Powers(_records(pg.raw, a), _records(pgg.raw, a)),
+            VerifierKey(v[:a], v[a:2 * a], v[2 * a:2 * a + G2_ARK_MONT_BYTES], v[2 * a + G2_ARK_MONT_BYTES:]))
+
+
+def load_kzg_setup(path: str = KZG_SETUP_FILE, n_log2: int = TAU_POWERS_LOG2):
+    """src/lib.rs:174-195 `load_kzg_setup() -> (Powers, VerifierKey)`; the per-point
+    deserialize_unchecked runs on the GPU. Raises KzgPotError where the reference unwrap()s."""
+    with open(path, "rb") as f:
+        return load_kzg_setup_buffer(f.read(), n_log2)
+
+
+def load_fastkzg_setup_buffer(data, n_log2: int = TAU_POWERS_LOG2):
+    n = 1 << n_log2
+    ptr, nbytes, keep = _buf(data)
+    pg = ctypes.create_string_buffer((2 * n - 1) * G1_ARK_MONT_BYTES)
+    pgg = ctypes.create_string_buffer(n * G1_ARK_MONT_BYTES)
+    hb = ctypes.create_string_buffer(2 * G2_ARK_MONT_BYTES)
+    ph = ctypes.create_string_buffer(n * G2_ARK_MONT_BYTES)
+    sec, idx = ctypes.c_int(-1), ctypes.c_int64(-1)
+    r = _lib.load().kzgpot_load_fastkzg_setup_buffer(ptr, nbytes, n_log2, pg, pgg, hb, ph, ctypes.byref(sec),
+                                                     ctypes.byref(idx))
+    del keep
+    _load_err(r, sec, idx)
+    b = G2_ARK_MONT_BYTES
+    powers_of_h = _records(ph.raw, b)
+    params = UniversalParams(_records(pg.raw, G1_ARK_MONT_BYTES), _records(pgg.raw, G1_ARK_MONT_BYTES),
+                             hb.raw[:b], ph.raw[b:2 * b], hb.raw[b:])
+    return params, powers_of_h
+
+
+def load_fastkzg_setup(path: str = KZG_SETUP_FILE, n_log2: int = TAU_POWERS_LOG2):
+    """src/lib.rs:197-228 `load_fastkzg_setup() -> (UniversalParams, Vec<G2Affine>)`. The default
+    path is KZG_SETUP_FILE because that is the file the reference opens here (lib.rs:198)."""
+    with open(path, "rb") as f:
+        return load_fastkzg_setup_buffer(f.read(), n_log2)
 
 
 def blake2b_hex(data: bytes) -> str:

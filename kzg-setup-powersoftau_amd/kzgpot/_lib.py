@@ -38,6 +38,16 @@ SIGNATURES = {
     "kzgpot_output_size": (ctypes.c_uint64, [ctypes.c_uint32, ctypes.c_int]),
     "kzgpot_preprocess": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_uint32, ctypes.c_int, intp, i64p]),
     "kzgpot_preprocess_buffer": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32, ctypes.c_int, intp, i64p]),
+    "kzgpot_g1_deserialize_unchecked": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, i64p]),
+    "kzgpot_g2_deserialize_unchecked": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, i64p]),
+    "kzgpot_g1_deserialize_unchecked_ex": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, i64p, ctypes.c_void_p]),
+    "kzgpot_g2_deserialize_unchecked_ex": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, i64p, ctypes.c_void_p]),
+    "kzgpot_g1_deserialize_unchecked_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "kzgpot_g2_deserialize_unchecked_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "kzgpot_load_kzg_setup": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, intp, i64p]),
+    "kzgpot_load_kzg_setup_buffer": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, intp, i64p]),
+    "kzgpot_load_fastkzg_setup": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, intp, i64p]),
+    "kzgpot_load_fastkzg_setup_buffer": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, intp, i64p]),
     "kzgpot_status_name": (ctypes.c_char_p, [ctypes.c_int]),
     "kzgpot_device_count": (ctypes.c_int, []),
     "kzgpot_version": (ctypes.c_char_p, []),

@@ -52,6 +52,8 @@ _DEV_FNS = {
     "g2_decompress": ("kzgpot_g2_decompress_dev", 96, 192),
     "g1_transcode": ("kzgpot_g1_transcode_uncompressed_dev", 96, 96),
     "g2_transcode": ("kzgpot_g2_transcode_uncompressed_dev", 192, 192),
+    "g1_load": ("kzgpot_g1_deserialize_unchecked_dev", 96, 104),   # no flags argument
+    "g2_load": ("kzgpot_g2_deserialize_unchecked_dev", 192, 200),
 }
 
 
@@ -65,8 +67,12 @@ def codec_dev(op: str, d_in: torch.Tensor, d_out: torch.Tensor, key: torch.Tenso
         raise ValueError(f"{op}: bad buffer sizes {d_in.numel()} / {d_out.numel()}")
     if not (d_in.is_cuda and d_out.is_cuda and key.is_cuda):
         raise ValueError("codec_dev needs device tensors")
-    rc = getattr(_lib.load(), fname)(d_in.data_ptr(), n, d_out.data_ptr(), flags, key.data_ptr(),
-                                     d_status.data_ptr() if d_status is not None else None, _stream())
+    st = d_status.data_ptr() if d_status is not None else None
+    fn = getattr(_lib.load(), fname)
+    if op.endswith("_load"):
+        rc = fn(d_in.data_ptr(), n, d_out.data_ptr(), key.data_ptr(), st, _stream())
+    else:
+        rc = fn(d_in.data_ptr(), n, d_out.data_ptr(), flags, key.data_ptr(), st, _stream())
     if rc:
         raise RuntimeError(f"{op}: launch failed ({rc})")
 

@@ -480,6 +480,72 @@ def g2_transcode_point(pairing192: bytes):
     return (st, None) if st else (OK, ark_g2_serialize(apt))
 
 
+# ----------------------------------------------------------------------------------------------
+# Loader mirror: load_kzg_setup / load_fastkzg_setup, src/lib.rs:174-228
+# ----------------------------------------------------------------------------------------------
+ARK_R = 1 << 384          # ark-ff 0.2 Fp384 Montgomery radix
+G1_ARK_MONT = 104         # GroupAffine<g1> in memory: x[6 x u64] y[6 x u64] infinity(u8) pad[7]
+G2_ARK_MONT = 200         # GroupAffine<g2>: x.c0 x.c1 y.c0 y.c1, infinity, pad
+
+
+def _ark_mont_bytes(v: int) -> bytes:
+    return (v * ARK_R % P).to_bytes(48, "little")
+
+
+def g1_deserialize_unchecked_point(ark96: bytes):
+    """ark-ec 0.2 `GroupAffine::<g1>::deserialize_unchecked` (src/lib.rs:180,183): coordinates < p
+    and SWFlags only — no curve, no subgroup check. Returns (status, in-memory 104-B record)."""
+    st, pt = ark_g1_deserialize_uncompressed(ark96, subgroup_check=False)
+    if st:
+        return st, None
+    x, y, inf = pt
+    return OK, _ark_mont_bytes(x) + _ark_mont_bytes(y) + bytes([1 if inf else 0]) + bytes(7)
+
+
+def g2_deserialize_unchecked_point(ark192: bytes):
+    """ark-ec 0.2 `GroupAffine::<g2>::deserialize_unchecked` (src/lib.rs:209-215)."""
+    st, pt = ark_g2_deserialize_uncompressed(ark192, subgroup_check=False)
+    if st:
+        return st, None
+    (x0, x1), (y0, y1), inf = pt
+    body = b"".join(_ark_mont_bytes(v) for v in (x0, x1, y0, y1))
+    return OK, body + bytes([1 if inf else 0]) + bytes(7)
+
+
+def _load_sections(data: bytes, plan):
+    """Sequential deserialize_unchecked over `plan` = [(g2?, count)] → (status, [section bytes]).
+    Raises on a short file (the reference's reader hits UnexpectedEof and unwraps)."""
+    off, outs = 0, []
+    for g2, count in plan:
+        rec = G2_UNCOMPRESSED if g2 else G1_UNCOMPRESSED
+        if off + count * rec > len(data):
+            raise ValueError("setup file too short")
+        fn = g2_deserialize_unchecked_point if g2 else g1_deserialize_unchecked_point
+        out, sts, bad = batch(fn, data[off:off + count * rec], rec, G2_ARK_MONT if g2 else G1_ARK_MONT)
+        if bad >= 0:
+            return sts[bad], outs
+        outs.append(out)
+        off += count * rec
+    return OK, outs
+
+
+def load_kzg_setup(data: bytes, n: int):
+    """src/lib.rs:174-195 → (status, (powers_of_g, powers_of_gamma_g, vk)) as in-memory records;
+    vk = g ‖ gamma_g ‖ h ‖ beta_h (VerifierKey::deserialize_unchecked)."""
+    st, outs = _load_sections(data, [(False, 2 * n - 1), (False, n), (False, 2), (True, 2)])
+    if st:
+        return st, None
+    return OK, (outs[0], outs[1], outs[2] + outs[3])
+
+
+def load_fastkzg_setup(data: bytes, n: int):
+    """src/lib.rs:197-228 → (status, (powers_of_g, powers_of_gamma_g, h ‖ beta_h, powers_of_h))."""
+    st, outs = _load_sections(data, [(False, 2 * n - 1), (False, n), (True, 2), (True, n)])
+    if st:
+        return st, None
+    return OK, tuple(outs)
+
+
 def batch(fn, data: bytes, rec: int, out_rec: int, **kw):
     """Apply a per-point function over a packed stream → (out bytes, statuses, first_bad)."""
     n = len(data) // rec

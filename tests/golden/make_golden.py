@@ -7,6 +7,8 @@ Vectors (all seeded, deterministic):
   g2_decompress.json   compressed G2 → ark uncompressed, positive + negative
   g1_transcode.json    pairing-uncompressed G1 → ark (read_g1, src/lib.rs:41-54), incl. off-curve
   g2_transcode.json    pairing-uncompressed G2 → ark (read_g2, src/lib.rs:56-80)
+  g1_load.json         ark uncompressed G1 → in-memory GroupAffine (deserialize_unchecked, the
+  g2_load.json         load_kzg_setup / load_fastkzg_setup loaders, src/lib.rs:174-228)
   transcript_n1024.bin a powersoftau response file for N = 2^10 (config 1), + expected digests of
                        the kgz / fastkgz outputs in transcript_n1024.json
 
@@ -229,10 +231,71 @@ def g2_transcode_vectors(rng):
     return V
 
 
+def g1_load_vectors(rng):
+    V = []
+
+    def add(b, note):
+        st, out = O.g1_deserialize_unchecked_point(b)
+        V.append(vec("g1l", b, st, out, note))
+
+    for i in range(16):
+        add(O.ark_g1_serialize((*O.g1_mul(O.G1_GEN, rng.randrange(1, O.R_ORDER)), False)), f"subgroup point {i}")
+    add(O.ark_g1_serialize(O.ARK_G1_ZERO), "ark zero (0, 1, infinity)")
+    q = O.g1_mul(O.G1_GEN, 7)
+    b = bytearray(O.ark_g1_serialize((*q, False)))
+    b[95] |= 0x40
+    add(bytes(b), "infinity flag with finite coordinates: kept as read")
+    b = bytearray(O.ark_g1_serialize((*q, False)))
+    b[95] |= 0x80
+    add(bytes(b), "PositiveY flag: ignored")
+    b = bytearray(O.ark_g1_serialize((*q, False)))
+    b[95] |= 0xC0
+    add(bytes(b), "both SW flags: UnexpectedFlags")
+    b = bytearray(O.ark_g1_serialize((*q, False)))
+    b[95] |= 0x20
+    add(bytes(b), "y >= p after flag removal")
+    for note, x in (("x = p", P), ("x = p - 1", P - 1), ("x = 2^384 - 1", (1 << 384) - 1)):
+        add(x.to_bytes(48, "little") + (3).to_bytes(48, "little"), note)
+    add(bytes(96), "(0, 0) unchecked: accepted")
+    for i in range(4):
+        add(rng.randrange(P).to_bytes(48, "little") + rng.randrange(P).to_bytes(48, "little"),
+            f"random off-curve (x, y) {i}: accepted (no curve check)")
+    add(O.ark_g1_serialize((*small_order_g1(rng, 11), False)), "order-11 point: accepted (no subgroup check)")
+    return V
+
+
+def g2_load_vectors(rng):
+    V = []
+
+    def add(b, note):
+        st, out = O.g2_deserialize_unchecked_point(b)
+        V.append(vec("g2l", b, st, out, note))
+
+    for i in range(8):
+        add(O.ark_g2_serialize((*O.g2_mul(O.G2_GEN, rng.randrange(1, O.R_ORDER)), False)), f"subgroup point {i}")
+    add(O.ark_g2_serialize(O.ARK_G2_ZERO), "ark zero")
+    q = O.g2_mul(O.G2_GEN, 3)
+    for note, byte, bit in (("infinity flag on y.c1", 191, 0x40), ("both SW flags", 191, 0xC0),
+                            ("PositiveY flag", 191, 0x80), ("top bit of y.c0: y.c0 >= p", 143, 0x80),
+                            ("top bit of x.c1: x.c1 >= p", 95, 0x80), ("bit 5 of y.c1: >= p", 191, 0x20)):
+        b = bytearray(O.ark_g2_serialize((*q, False)))
+        b[byte] |= bit
+        add(bytes(b), note)
+    add(b"".join(rng.randrange(P).to_bytes(48, "little") for _ in range(4)), "random off-curve: accepted")
+    return V
+
+
 def main():
     rng = random.Random(20261015)
     for name, fn in (("g1_decompress", g1_vectors), ("g2_decompress", g2_vectors),
                      ("g1_transcode", g1_transcode_vectors), ("g2_transcode", g2_transcode_vectors)):
+        V = fn(rng)
+        with open(os.path.join(HERE, name + ".json"), "w") as f:
+            json.dump({"generator": "tests/golden/make_golden.py", "oracle": "oracle/kzgpot_oracle.py",
+                       "vectors": V}, f, indent=0)
+        print(name, len(V), "vectors;", sum(v["status"] == 0 for v in V), "accepted")
+    rng = random.Random(20261016)  # separate stream: the loader vectors came later
+    for name, fn in (("g1_load", g1_load_vectors), ("g2_load", g2_load_vectors)):
         V = fn(rng)
         with open(os.path.join(HERE, name + ".json"), "w") as f:
             json.dump({"generator": "tests/golden/make_golden.py", "oracle": "oracle/kzgpot_oracle.py",
@@ -251,6 +314,12 @@ def main():
         "kgz_head_hex": kgz[:192].hex(), "kgz_tail_hex": kgz[-576:].hex(),
         "fastkgz_tail_hex": fast[-192:].hex(),
     }
+    st, loaded = O.load_kzg_setup(kgz, n)
+    assert st == 0
+    meta["load_kzg_blake2b"] = O.blake2b_hex(b"".join(loaded))
+    st, loaded = O.load_fastkzg_setup(fast, n)
+    assert st == 0
+    meta["load_fastkzg_blake2b"] = O.blake2b_hex(b"".join(loaded))
     with open(os.path.join(HERE, "transcript_n1024.json"), "w") as f:
         json.dump(meta, f, indent=1)
     print("transcript", len(tr), "kgz", len(kgz), "fastkgz", len(fast))

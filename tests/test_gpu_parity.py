@@ -149,3 +149,74 @@ def test_read_g1_read_g2_mirror(gpu):
     bad = next(v for v in golden("g1_transcode") if v["status"] == 5)
     with pytest.raises(gpu.KzgPotError):
         gpu.read_g1(io.BytesIO(bytes.fromhex(bad["in"])))
+
+
+# ------------------------------------------------------------------ loader mirror (§8f 2)
+@pytest.mark.parametrize("name,g2,rin,rout", [("g1_load", False, 96, 104), ("g2_load", True, 192, 200)])
+def test_load_golden_vectors(gpu, name, g2, rin, rout):
+    vecs = golden(name)
+    for v in vecs:  # one by one: status class and bytes
+        r = gpu.deserialize_unchecked(bytes.fromhex(v["in"]), g2=g2, want_status=True)
+        assert r.status[0] == v["status"], v["note"]
+        assert r.out == (bytes.fromhex(v["out"]) if v["out"] else bytes(rout)), v["note"]
+    r = gpu.deserialize_unchecked(b"".join(bytes.fromhex(v["in"]) for v in vecs), g2=g2, want_status=True)
+    first = next(i for i, v in enumerate(vecs) if v["status"])
+    assert r.first_bad == first and r.ret == -vecs[first]["status"]
+    assert r.out == b"".join(bytes.fromhex(v["out"]) if v["out"] else bytes(rout) for v in vecs)
+
+
+def test_load_setup_config1(gpu, tmp_path):
+    meta = json.load(open(os.path.join(GOLDEN, "transcript_n1024.json")))
+    tr = open(os.path.join(GOLDEN, "transcript_n1024.bin"), "rb").read()
+    kgz = gpu.preprocess_buffer(tr, 10, gpu.MODE_KZG)
+    powers, vk = gpu.load_kzg_setup_buffer(kgz, 10)
+    assert powers.powers_of_g.shape == (2047, 104) and powers.powers_of_gamma_g.shape == (1024, 104)
+    blob = powers.powers_of_g.tobytes() + powers.powers_of_gamma_g.tobytes() + vk.g + vk.gamma_g + vk.h + vk.beta_h
+    assert hashlib.blake2b(blob).hexdigest() == meta["load_kzg_blake2b"]
+    assert vk.g == powers.powers_of_g[0].tobytes()  # g = τG1[0]
+    path = tmp_path / "kzg_setup"
+    path.write_bytes(kgz + b"trailing bytes are ignored")
+    p2, vk2 = gpu.load_kzg_setup(str(path), 10)
+    assert p2.powers_of_g.tobytes() == powers.powers_of_g.tobytes() and vk2 == vk
+
+    fast = gpu.preprocess_buffer(tr, 10, gpu.MODE_FASTKZG)
+    params, powers_of_h = gpu.load_fastkzg_setup_buffer(fast, 10)
+    blob = (params.powers_of_g.tobytes() + params.powers_of_gamma_g.tobytes() + params.h + params.beta_h_read
+            + powers_of_h.tobytes())
+    assert hashlib.blake2b(blob).hexdigest() == meta["load_fastkzg_blake2b"]
+    assert params.beta_h == powers_of_h[1].tobytes() and params.h == powers_of_h[0].tobytes()
+
+
+def test_load_setup_rejections(gpu):
+    tr = open(os.path.join(GOLDEN, "transcript_n1024.bin"), "rb").read()
+    kgz = bytearray(gpu.preprocess_buffer(tr, 10, gpu.MODE_KZG))
+    with pytest.raises(gpu.KzgPotError) as e:
+        gpu.load_kzg_setup_buffer(bytes(kgz[:-1]), 10)
+    assert e.value.code == -103
+    off = 2047 * 96 + 5 * 96  # powers_of_gamma_g[5].y top byte: both SW flags
+    kgz[off + 95] |= 0xC0
+    with pytest.raises(gpu.KzgPotError) as e:
+        gpu.load_kzg_setup_buffer(bytes(kgz), 10)
+    assert e.value.code == -6 and e.value.section == 1 and e.value.first_bad == 5
+    kgz[off + 95] &= 0x3F
+    kgz[12 * 96:12 * 96 + 48] = b"\xff" * 48  # powers_of_g[12].x >= p
+    with pytest.raises(gpu.KzgPotError) as e:
+        gpu.load_kzg_setup_buffer(bytes(kgz), 10)
+    assert e.value.code == -3 and e.value.section == 0 and e.value.first_bad == 12
+
+
+def test_load_dev_api(gpu):
+    import torch
+
+    from kzgpot import device
+
+    vecs = [v for v in golden("g1_load")]
+    data = b"".join(bytes.fromhex(v["in"]) for v in vecs)
+    d_in = torch.frombuffer(bytearray(data), dtype=torch.uint8).cuda()
+    d_out = torch.empty(len(vecs) * 104, dtype=torch.uint8, device="cuda")
+    key = torch.empty(1, dtype=torch.int64, device="cuda")
+    device.codec_dev("g1_load", d_in, d_out, key)
+    torch.cuda.synchronize()
+    first = next(i for i, v in enumerate(vecs) if v["status"])
+    assert device.read_key(key) == (first << 8) | vecs[first]["status"]
+    assert d_out.cpu().numpy().tobytes() == b"".join(bytes.fromhex(v["out"]) if v["out"] else bytes(104) for v in vecs)

@@ -8,6 +8,7 @@ Anchors (the reference ships no vectors for this path — SURVEY.md §4, §8c):
     N = 2^10 transcript pipelines;
   * the reference's own constants (digests, sizes) reproduced.
 """
+import ctypes
 import hashlib
 import json
 import os
@@ -133,3 +134,46 @@ def test_transcript_rejections(oracle_lib):
     r = oracle_lib.oracle_preprocess(bytes(tr[:-1]), ctypes.c_size_t(len(tr) - 1), ctypes.c_uint64(n), 0, out, 2,
                                      ctypes.byref(sec), ctypes.byref(idx))
     assert r == -103
+
+
+@pytest.mark.parametrize("name,fn", [("g1_load", O.g1_deserialize_unchecked_point),
+                                     ("g2_load", O.g2_deserialize_unchecked_point)])
+def test_python_oracle_reproduces_load_golden(name, fn):
+    for v in golden(name):
+        st, out = fn(bytes.fromhex(v["in"]))
+        assert st == v["status"], v["note"]
+        assert (out.hex() if out else None) == v["out"], v["note"]
+
+
+def test_load_golden_semantics():
+    """Spot-check the loader vectors against ark's definitions directly: Montgomery R = 2^384,
+    infinity byte, padding."""
+    for v in golden("g1_load"):
+        if v["status"]:
+            continue
+        inp, out = bytes.fromhex(v["in"]), bytes.fromhex(v["out"])
+        x = int.from_bytes(inp[:48], "little")
+        y = int.from_bytes(inp[48:96], "little") & ((1 << 382) - 1)
+        assert int.from_bytes(out[:48], "little") == x * (1 << 384) % O.P
+        assert int.from_bytes(out[48:96], "little") == y * (1 << 384) % O.P
+        assert out[96] == (inp[95] >> 6 & 1) and out[97:] == bytes(7)
+
+
+def test_load_setup_digests(oracle_lib):
+    """load_kzg_setup / load_fastkzg_setup on the config-1 outputs (made by the C oracle) against
+    the committed digests of the oracle loaders' records."""
+    meta = json.load(open(os.path.join(GOLDEN, "transcript_n1024.json")))
+    tr = open(os.path.join(GOLDEN, "transcript_n1024.bin"), "rb").read()
+    n = meta["n"]
+    for fast, key in ((0, "load_kzg_blake2b"), (1, "load_fastkzg_blake2b")):
+        size = oracle_lib.oracle_output_size(ctypes.c_uint64(n), fast)
+        out = ctypes.create_string_buffer(size)
+        sec, idx = ctypes.c_int(-1), ctypes.c_int64(-1)
+        assert oracle_lib.oracle_preprocess(tr, ctypes.c_size_t(len(tr)), ctypes.c_uint64(n), fast, out, 8,
+                                            ctypes.byref(sec), ctypes.byref(idx)) == 0
+        loader = O.load_fastkzg_setup if fast else O.load_kzg_setup
+        st, parts = loader(out.raw, n)
+        assert st == 0
+        assert hashlib.blake2b(b"".join(parts)).hexdigest() == meta[key]
+    with pytest.raises(ValueError):
+        O.load_kzg_setup(b"\x00" * 100, n)
