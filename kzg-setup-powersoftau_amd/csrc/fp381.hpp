@@ -172,6 +172,12 @@ KZG_DEV void fp_reduce_canon(fp& r, const fp& a) {
 #undef KZG_RED_STEP
   r = x;
 }
+// normalized, value < 2 p -> canonical (one conditional subtraction)
+KZG_DEV void fp_reduce_once(fp& r, const fp& a) {
+  fp d;
+  const bool b = fp_sub_const_borrow(d, a, FP_P);
+  fp_select(r, b, a, d);
+}
 // any value with limbs < 2^32 - 16 and value < 256 p -> canonical
 KZG_DEV void fp_canon(fp& r, const fp& a) {
   fp n;
@@ -265,13 +271,14 @@ KZG_DEV void fp_to_mont(fp& r, const fp& canon) {
   fp_set(r2, FP_R2);
   fp_mul(r, canon, r2);
 }
-// Montgomery -> canonical (normalized, [0, p))
+// Montgomery -> canonical (normalized, [0, p)). For normalized a (< 2^392 = R) the Montgomery
+// product a * 1 is (a + m p) / R < 1 + p, so one conditional subtraction finishes it.
 KZG_DEV void fp_from_mont(fp& canon, const fp& a) {
   fp one;
   fp_zero(one);
   one.v[0] = 1;
   fp_mul(canon, a, one);
-  fp_reduce_canon(canon, canon);
+  fp_reduce_once(canon, canon);
 }
 
 // r = a^((p-3)/4): fixed sliding-window schedule (tools/gen_constants.py), identical for every

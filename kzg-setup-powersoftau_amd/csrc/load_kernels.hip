@@ -12,7 +12,8 @@
 // padding to 8 B: G1 104 B (x 48 | y 48 | inf 1 | pad 7), G2 200 B (x.c0 | x.c1 | y.c0 | y.c1 |
 // inf | pad). Rejected points are zero-filled.
 //
-// HBM-bound: 96 B in + 104 B out per G1 point against 2 Fp multiplies.
+// HBM-bound: 96 B in + 104 B out per G1 point against 2 Fp multiplies; global traffic is staged
+// through LDS so that it is fully coalesced.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -22,104 +23,99 @@
 
 namespace kzgpot {
 
-// canonical words (< p) -> ark Montgomery words: x 2^384 mod p
+// canonical words (< p) -> ark Montgomery words: x 2^384 mod p (one multiply + one conditional
+// subtraction: the product of a canonical x and FP_ARK_R is < 2p, tests/test_field_bounds.py)
 KZG_DEV void words_to_ark_mont(words& out, const words& w) {
   fp x, k;
   fp_from_words(x, w);
   fp_set(k, FP_ARK_R);
   fp_mul(x, x, k);
-  fp_reduce_canon(x, x);
+  fp_reduce_once(x, x);
   fp_to_words(out, x);
 }
 
-KZG_DEV void store_u64x(uint2* dst, const words& w) {  // 48 B at an 8-B aligned address
-#pragma unroll
-  for (int k = 0; k < 6; k++) dst[k] = make_uint2(w[2 * k], w[2 * k + 1]);
-}
+// One block handles BLK consecutive points. Records are packed at 96 / 192 B (in) and 104 / 200
+// B (out), which lane-per-record accesses would touch at a 96-200 B stride; instead the block
+// stages its whole input and output slab through LDS so that every global access is a
+// contiguous, fully coalesced 16-B-per-lane sweep.
+//   NC = coordinates per point (2: G1, 4: G2); the last one carries the SWFlags.
+template <int NC, int BLK>
+__global__ void __launch_bounds__(BLK) k_load(const uint4* __restrict__ in, uint4* __restrict__ out, uint64_t n,
+                                              unsigned long long* __restrict__ first_bad,
+                                              uint8_t* __restrict__ status) {
+  constexpr int RIN = 48 * NC, ROUT = 48 * NC + 8;
+  static_assert(RIN % 16 == 0 && (BLK * ROUT) % 16 == 0 && ROUT % 8 == 0, "slab alignment");
+  __shared__ uint4 slab[BLK * ROUT / 16];
+  const uint64_t base = (uint64_t)blockIdx.x * BLK;
+  const int cnt = (int)((n - base) < (uint64_t)BLK ? (n - base) : (uint64_t)BLK);
+  const int t = threadIdx.x;
 
-__global__ void __launch_bounds__(kBlock) k_g1_load(const uint4* __restrict__ in, uint2* __restrict__ out,
-                                                    uint64_t n, unsigned long long* __restrict__ first_bad,
-                                                    uint8_t* __restrict__ status) {
-  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (i >= n) return;
-  words x, y;
-  load_le(x, in + i * 6);
-  load_le(y, in + i * 6 + 3);
-  const uint32_t yb = y[11] >> 24;
-  const bool fpos = yb & 0x80u, finf = yb & 0x40u;
-  y[11] &= 0x3fffffffu;
-  int st = 0;
-  if (words_geq_p(x)) st = 3;
-  else if (fpos && finf) st = 6;
-  else if (words_geq_p(y)) st = 3;
-  uint2* dst = out + i * 13;
-  if (st) {
-#pragma unroll
-    for (int k = 0; k < 13; k++) dst[k] = make_uint2(0, 0);
-  } else {
-    words m;
-    words_to_ark_mont(m, x);
-    store_u64x(dst, m);
-    words_to_ark_mont(m, y);
-    store_u64x(dst + 6, m);
-    dst[12] = make_uint2(finf ? 1u : 0u, 0u);
-  }
-  report(i, st, first_bad, status);
-}
+  const uint4* src = in + base * (RIN / 16);
+  const int nin = cnt * (RIN / 16);
+  for (int k = t; k < nin; k += BLK) slab[k] = src[k];
+  __syncthreads();
 
-__global__ void __launch_bounds__(kBlock) k_g2_load(const uint4* __restrict__ in, uint2* __restrict__ out,
-                                                    uint64_t n, unsigned long long* __restrict__ first_bad,
-                                                    uint8_t* __restrict__ status) {
-  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (i >= n) return;
-  const uint4* rec = in + i * 12;
   int st = 0;
-  bool finf;
-  {
+  bool finf = false;
+  words res[NC];
+  if (t < cnt) {
+    const uint4* rec = slab + t * (RIN / 16);
     words c;
-    load_le(c, rec + 9);  // y.c1 carries the flags
+    load_le(c, rec + 3 * (NC - 1));
     const uint32_t yb = c[11] >> 24;
     const bool fpos = yb & 0x80u;
     finf = yb & 0x40u;
-    c[11] &= 0x3fffffffu;
-    words a;
-    load_le(a, rec);
-    if (words_geq_p(a)) st = 3;
-    load_le(a, rec + 3);
-    if (!st && words_geq_p(a)) st = 3;
-    load_le(a, rec + 6);
-    if (!st && words_geq_p(a)) st = 3;
-    if (!st && fpos && finf) st = 6;
-    if (!st && words_geq_p(c)) st = 3;
-  }
-  uint2* dst = out + i * 25;
-  if (st) {
-#pragma unroll 1
-    for (int k = 0; k < 25; k++) dst[k] = make_uint2(0, 0);
-  } else {
-#pragma unroll 1
-    for (int c = 0; c < 4; c++) {
-      words w, m;
-      load_le(w, rec + 3 * c);
-      if (c == 3) w[11] &= 0x3fffffffu;
-      words_to_ark_mont(m, w);
-      store_u64x(dst + 6 * c, m);
+    // ark reads the coordinates in order; the flags are parsed before the last one's range check
+#pragma unroll
+    for (int k = 0; k < NC - 1; k++) {
+      words a;
+      load_le(a, rec + 3 * k);
+      if (!st && words_geq_p(a)) st = 3;
     }
-    dst[24] = make_uint2(finf ? 1u : 0u, 0u);
+    if (!st && fpos && finf) st = 6;
+    c[11] &= 0x3fffffffu;
+    if (!st && words_geq_p(c)) st = 3;
+#pragma clang loop unroll(full)
+    for (int k = 0; k < NC; k++) {
+      words a;
+      load_le(a, rec + 3 * k);
+      if (k == NC - 1) a[11] &= 0x3fffffffu;
+      words_to_ark_mont(res[k], a);
+    }
   }
-  report(i, st, first_bad, status);
+  __syncthreads();  // every lane has read its input record: the slab becomes the output slab
+  if (t < cnt) {
+    uint2* dst = (uint2*)slab + t * (ROUT / 8);
+#pragma unroll
+    for (int k = 0; k < NC; k++)
+#pragma unroll
+      for (int j = 0; j < 6; j++) dst[6 * k + j] = st ? make_uint2(0, 0) : make_uint2(res[k][2 * j], res[k][2 * j + 1]);
+    dst[6 * NC] = make_uint2((!st && finf) ? 1u : 0u, 0u);
+    report(base + t, st, first_bad, status);
+  }
+  __syncthreads();
+  if (cnt == BLK) {
+    uint4* dst = (uint4*)((uint8_t*)out + base * ROUT);  // BLK * ROUT is a multiple of 16
+    for (int k = t; k < BLK * ROUT / 16; k += BLK) dst[k] = slab[k];
+  } else {  // ragged tail block: the slab ends on an 8-B boundary
+    uint2* dst = (uint2*)out + base * (ROUT / 8);
+    const uint2* s2 = (const uint2*)slab;
+    for (int k = t; k < cnt * (ROUT / 8); k += BLK) dst[k] = s2[k];
+  }
 }
 
 hipError_t launch_load(bool g2, const void* d_in, void* d_out, uint64_t n, unsigned long long* d_first_bad,
                        uint8_t* d_status, hipStream_t stream) {
   if (n == 0) return hipSuccess;
-  const dim3 grid((unsigned)((n + kBlock - 1) / kBlock)), block(kBlock);
-  if (g2)
-    hipLaunchKernelGGL(k_g2_load, grid, block, 0, stream, (const uint4*)d_in, (uint2*)d_out, n, d_first_bad,
-                       d_status);
-  else
-    hipLaunchKernelGGL(k_g1_load, grid, block, 0, stream, (const uint4*)d_in, (uint2*)d_out, n, d_first_bad,
-                       d_status);
+  if (g2) {
+    constexpr int B = 128;
+    hipLaunchKernelGGL((k_load<4, B>), dim3((unsigned)((n + B - 1) / B)), dim3(B), 0, stream, (const uint4*)d_in,
+                       (uint4*)d_out, n, d_first_bad, d_status);
+  } else {
+    constexpr int B = 256;
+    hipLaunchKernelGGL((k_load<2, B>), dim3((unsigned)((n + B - 1) / B)), dim3(B), 0, stream, (const uint4*)d_in,
+                       (uint4*)d_out, n, d_first_bad, d_status);
+  }
   return hipGetLastError();
 }
 

@@ -134,6 +134,19 @@ def canon_ok(a, name="canon"):
         raise BoundError(f"{name}: canon precondition violated {a!r}")
 
 
+def reduce_once_ok(a, name="reduce_once"):
+    """fp_reduce_once precondition: normalized, value < 2 p."""
+    if any(l > LM for l in a.limbs) or a.val >= 2:
+        raise BoundError(f"{name}: one conditional subtraction cannot canonicalize {a!r}")
+
+
+def from_mont_ok(a, name="from_mont"):
+    """fp_from_mont: a must be normalized (a < R); mul(a, 1) < p + 1 then reduce_once."""
+    if any(l > LM for l in a.limbs):
+        raise BoundError(f"{name}: input not normalized {a!r}")
+    reduce_once_ok(mul(a, normalized(Fraction(1, 10**9)), name), name)
+
+
 def vmax(*vs):
     return V([max(x) for x in zip(*(v.limbs for v in vs))], max(v.val for v in vs), "join")
 

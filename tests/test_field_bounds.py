@@ -45,7 +45,7 @@ def test_sqrt_chain_inputs():
     t = _pow_pm3d4(a)
     y = M.mul(t, a, "y")
     M.canon_ok(M.subk(M.mul(y, y), a, "KB_64_31"), "fp_eq")
-    M.canon_ok(M.mul(y, M.normalized(Fraction(1, 10**6))), "from_mont")
+    M.from_mont_ok(y)
 
 
 def _fp2_mont(v):
@@ -73,7 +73,7 @@ def test_fp2_sqrt_and_psi():
     y2 = M.f2_sqr(y)
     M.canon_ok(M.sub_red(y2.c0, a.c0), "y^2 == a")
     for c in (y.c0, y.c1):
-        M.canon_ok(M.mul(c, M.normalized(Fraction(1, 10**6))), "from_mont")
+        M.from_mont_ok(c)
     # G2 check kernel: on-curve test and psi(P) with canonical (range-checked) inputs
     pm = M.V2(_fp2_mont(1), _fp2_mont(1))
     lhs = M.f2_sqr(pm)
@@ -116,5 +116,11 @@ def test_synth_madd_chain():
     zi = _pow_pm3d4(Z)
     zi = M.mul(M.mul(M.mul(zi, zi), zi), Z, "inv")
     z2 = M.mul(zi, zi)
-    M.canon_ok(M.mul(X, z2), "x")
-    M.canon_ok(M.mul(Y, M.mul(z2, zi)), "y")
+    M.from_mont_ok(M.mul(X, z2), "x")
+    M.from_mont_ok(M.mul(Y, M.mul(z2, zi)), "y")
+
+
+def test_loader_conversion():
+    """load_kernels.hip words_to_ark_mont: canonical x (< p) times FP_ARK_R, one reduction."""
+    k = M.const(M.C["FP_ARK_R"])
+    M.reduce_once_ok(M.mul(M.normalized(1), k))
