@@ -110,6 +110,20 @@ int kzgpot_preprocess(const char* transcript_path, const char* out_path, int mod
 /* Same, on in-memory buffers (out must hold kzgpot_output_size bytes). */
 int kzgpot_preprocess_buffer(const uint8_t* transcript, size_t len, uint8_t* out, int mode, uint32_t n_log2,
                              int n_gpus, int* bad_section, int64_t* bad_index);
+/* With the BLAKE2b-512 digests (src/lib.rs:129; the reference checks the transcript against
+ * POWERSOFTAU_DIGEST, preprocess-kgz.rs:19,51-61, and publishes the outputs' digests,
+ * src/lib.rs:21-22). Hashing runs on host threads beside the GPU pass: the transcript from the
+ * start, the output section by section as the GPU finishes it. expect_transcript_digest (128 hex
+ * chars, may be NULL): a mismatch returns KZGPOT_E_DIGEST (and no output file is written).
+ * transcript_digest / output_digest (may be NULL): receive 128 hex chars + NUL. */
+int kzgpot_preprocess_ex(const char* transcript_path, const char* out_path, int mode, uint32_t n_log2, int n_gpus,
+                         const char* expect_transcript_digest, char* transcript_digest, char* output_digest,
+                         int* bad_section, int64_t* bad_index);
+int kzgpot_preprocess_buffer_ex(const uint8_t* transcript, size_t len, uint8_t* out, int mode, uint32_t n_log2,
+                                int n_gpus, const char* expect_transcript_digest, char* transcript_digest,
+                                char* output_digest, int* bad_section, int64_t* bad_index);
+/* BLAKE2b-512 (unkeyed, 64-byte digest) of a host buffer — blake2b_simd::State::new() (src/lib.rs:129). */
+int kzgpot_blake2b(const uint8_t* data, size_t len, uint8_t* digest64);
 
 /* ---------------------------------------------------------------- loader mirror (next-row §8f 2) */
 /* ark-ec 0.2 GroupAffine in memory (what `deserialize_unchecked` returns): each Fp as 6 LE u64 in

@@ -1,0 +1,113 @@
+// BLAKE2b-512 (RFC 7693), unkeyed — the digest the reference checks with blake2b_simd
+// (`State::new().update(data).finalize()`, src/lib.rs:129, preprocess-kgz.rs:51-61). Host code:
+// hashing is a sequential byte stream, so it runs on a CPU thread beside the GPU pass.
+#include "blake2b.hpp"
+
+#include <string.h>
+
+namespace kzgpot {
+namespace {
+
+constexpr uint64_t kIV[8] = {0x6a09e667f3bcc908ull, 0xbb67ae8584caa73bull, 0x3c6ef372fe94f82bull,
+                             0xa54ff53a5f1d36f1ull, 0x510e527fade682d1ull, 0x9b05688c2b3e6c1full,
+                             0x1f83d9abfb41bd6bull, 0x5be0cd19137e2179ull};
+constexpr uint8_t kSigma[12][16] = {
+    {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15}, {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3},
+    {11, 8, 12, 0, 5, 2, 15, 13, 10, 14, 3, 6, 7, 1, 9, 4}, {7, 9, 3, 1, 13, 12, 11, 14, 2, 6, 5, 10, 4, 0, 15, 8},
+    {9, 0, 5, 7, 2, 4, 10, 15, 14, 1, 11, 12, 6, 8, 3, 13}, {2, 12, 6, 10, 0, 11, 8, 3, 4, 13, 7, 5, 15, 14, 1, 9},
+    {12, 5, 1, 15, 14, 13, 4, 10, 0, 7, 6, 3, 9, 2, 8, 11}, {13, 11, 7, 14, 12, 1, 3, 9, 5, 0, 15, 4, 8, 6, 2, 10},
+    {6, 15, 14, 9, 11, 3, 0, 8, 12, 2, 13, 7, 1, 4, 10, 5}, {10, 2, 8, 4, 7, 6, 1, 5, 15, 11, 9, 14, 3, 12, 13, 0},
+    {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15}, {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3}};
+
+inline uint64_t rotr(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+
+inline uint64_t load64(const uint8_t* p) {
+  uint64_t v;
+  memcpy(&v, p, 8);  // little-endian host (x86-64 / aarch64)
+  return v;
+}
+
+}  // namespace
+
+void Blake2b::init() {
+  for (int i = 0; i < 8; i++) h_[i] = kIV[i];
+  h_[0] ^= 0x01010000ull ^ 64;  // digest length 64, no key, fanout 1, depth 1
+  t_ = 0;
+  n_ = 0;
+}
+
+void Blake2b::compress(const uint8_t* block, bool last) {
+  uint64_t m[16], v[16];
+  for (int i = 0; i < 16; i++) m[i] = load64(block + 8 * i);
+  for (int i = 0; i < 8; i++) v[i] = h_[i], v[i + 8] = kIV[i];
+  v[12] ^= (uint64_t)t_;
+  v[13] ^= (uint64_t)(t_ >> 64);
+  if (last) v[14] = ~v[14];
+#define KZG_G(a, b, c, d, x, y)   \
+  a = a + b + x;                  \
+  d = rotr(d ^ a, 32);            \
+  c = c + d;                      \
+  b = rotr(b ^ c, 24);            \
+  a = a + b + y;                  \
+  d = rotr(d ^ a, 16);            \
+  c = c + d;                      \
+  b = rotr(b ^ c, 63);
+  for (int r = 0; r < 12; r++) {
+    const uint8_t* s = kSigma[r];
+    KZG_G(v[0], v[4], v[8], v[12], m[s[0]], m[s[1]]);
+    KZG_G(v[1], v[5], v[9], v[13], m[s[2]], m[s[3]]);
+    KZG_G(v[2], v[6], v[10], v[14], m[s[4]], m[s[5]]);
+    KZG_G(v[3], v[7], v[11], v[15], m[s[6]], m[s[7]]);
+    KZG_G(v[0], v[5], v[10], v[15], m[s[8]], m[s[9]]);
+    KZG_G(v[1], v[6], v[11], v[12], m[s[10]], m[s[11]]);
+    KZG_G(v[2], v[7], v[8], v[13], m[s[12]], m[s[13]]);
+    KZG_G(v[3], v[4], v[9], v[14], m[s[14]], m[s[15]]);
+  }
+#undef KZG_G
+  for (int i = 0; i < 8; i++) h_[i] ^= v[i] ^ v[i + 8];
+}
+
+void Blake2b::update(const uint8_t* p, size_t len) {
+  // the final block is compressed in finalize(), so keep up to 128 bytes buffered
+  while (len > 0) {
+    if (n_ == 128) {
+      t_ += 128;
+      compress(buf_, false);
+      n_ = 0;
+    }
+    if (n_ == 0) {
+      while (len > 128) {  // whole blocks straight from the input
+        t_ += 128;
+        compress(p, false);
+        p += 128;
+        len -= 128;
+      }
+    }
+    const size_t take = len < 128 - n_ ? len : 128 - n_;
+    memcpy(buf_ + n_, p, take);
+    n_ += take;
+    p += take;
+    len -= take;
+  }
+}
+
+void Blake2b::finalize(uint8_t out[64]) {
+  t_ += n_;
+  memset(buf_ + n_, 0, 128 - n_);
+  compress(buf_, true);
+  memcpy(out, h_, 64);
+}
+
+void blake2b_512(const uint8_t* data, size_t len, uint8_t out[64]) {
+  Blake2b h;
+  h.update(data, len);
+  h.finalize(out);
+}
+
+void to_hex(const uint8_t d[64], char hex[129]) {
+  static const char* k = "0123456789abcdef";
+  for (int i = 0; i < 64; i++) hex[2 * i] = k[d[i] >> 4], hex[2 * i + 1] = k[d[i] & 15];
+  hex[128] = 0;
+}
+
+}  // namespace kzgpot

@@ -7,10 +7,14 @@
 #include <string.h>
 
 #include <algorithm>
+#include <condition_variable>
+#include <deque>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <vector>
 
+#include "blake2b.hpp"
 #include "codec.hpp"
 
 using namespace kzgpot;
@@ -181,29 +185,101 @@ uint64_t kzgpot_output_size(uint32_t n_log2, int mode) {
                                      : (2 * n - 1) * 96 + n * 96 + 576;
 }
 
-int kzgpot_preprocess_buffer(const uint8_t* tr, size_t len, uint8_t* out, int mode, uint32_t n_log2, int n_gpus,
-                             int* bad_section, int64_t* bad_index) {
+}  // extern "C"
+
+namespace {
+
+// Hashes byte ranges in submission order on its own thread (BLAKE2b is one sequential stream), so
+// the output digest is computed while the GPU is still decoding later sections.
+class OrderedHasher {
+ public:
+  OrderedHasher() : th_([this] { run(); }) {}
+  ~OrderedHasher() { finish(nullptr); }
+  void push(const uint8_t* p, size_t n) {
+    std::lock_guard<std::mutex> l(mu_);
+    q_.emplace_back(p, n);
+    cv_.notify_one();
+  }
+  // waits for every pushed range; writes the digest if out != nullptr
+  void finish(uint8_t* out) {
+    {
+      std::lock_guard<std::mutex> l(mu_);
+      if (done_) return;
+      done_ = true;
+      cv_.notify_one();
+    }
+    th_.join();
+    if (out) h_.finalize(out);
+  }
+
+ private:
+  void run() {
+    for (;;) {
+      std::pair<const uint8_t*, size_t> item;
+      {
+        std::unique_lock<std::mutex> l(mu_);
+        cv_.wait(l, [this] { return done_ || !q_.empty(); });
+        if (q_.empty()) return;
+        item = q_.front();
+        q_.pop_front();
+      }
+      h_.update(item.first, item.second);
+    }
+  }
+  Blake2b h_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<std::pair<const uint8_t*, size_t>> q_;
+  bool done_ = false;
+  std::thread th_;
+};
+
+int preprocess_impl(const uint8_t* tr, size_t len, uint8_t* out, int mode, uint32_t n_log2, int n_gpus,
+                    const char* expect_in_hex, char* in_hex, char* out_hex, int* bad_section,
+                    int64_t* bad_index) {
   if (bad_section) *bad_section = -1;
   if (bad_index) *bad_index = -1;
   if (!tr || !out || n_log2 > 30 || (mode != KZGPOT_MODE_KZG && mode != KZGPOT_MODE_FASTKZG))
     return KZGPOT_E_INVALID_ARG;
+  if (expect_in_hex && strlen(expect_in_hex) != 128) return KZGPOT_E_INVALID_ARG;
   if (len != kzgpot_contribution_size(n_log2)) return KZGPOT_E_SIZE;
   const int ndev = device_count();
   if (ndev <= 0) return KZGPOT_E_DEVICE;
   if (n_gpus <= 0 || n_gpus > ndev) n_gpus = ndev;
   const uint64_t n = 1ull << n_log2;
+
+  // transcript digest (download_parameters' check, preprocess-kgz.rs:51-61) beside the GPU pass
+  uint8_t in_digest[64];
+  std::thread in_hash;
+  const bool want_in = expect_in_hex || in_hex;
+  if (want_in) in_hash = std::thread([&] { blake2b_512(tr, len, in_digest); });
+  std::unique_ptr<OrderedHasher> out_hash(out_hex ? new OrderedHasher() : nullptr);
+
   // powersoftau Accumulator section order (after the 64-B hash)
   const uint64_t cnt[5] = {2 * n - 1, n, n, n, 1};
   const bool g2[5] = {false, true, false, false, true};
   // read back by read_g1/read_g2 (checked) in each binary: kgz τG1, τG2, ατG1; fastkgz + βτG1
   const bool checked[5] = {true, true, true, mode == KZGPOT_MODE_FASTKZG, false};
-  std::vector<std::vector<uint8_t>> sec(5);
+  // output layout (A7): τG1 and ατG1 are decoded straight into their place in `out`; fastkzg's
+  // powers_of_h (= τG2) too; the rest goes to scratch
+  const uint64_t off_gamma = (2 * n - 1) * 96, off_tail = off_gamma + n * 96;
+  std::vector<std::vector<uint8_t>> scratch(5);
+  uint8_t* dst[5];
+  for (int s = 0; s < 5; s++) {
+    const uint64_t rout = g2[s] ? 192 : 96;
+    if (s == 0) dst[s] = out;
+    else if (s == 2) dst[s] = out + off_gamma;
+    else if (s == 1 && mode == KZGPOT_MODE_FASTKZG) dst[s] = out + off_tail + 2 * 192;
+    else {
+      scratch[s].resize(cnt[s] * rout);
+      dst[s] = scratch[s].data();
+    }
+  }
   int ret = 0;
   const uint8_t* p = tr + 64;
-  for (int s = 0; s < 5; s++) {
+  for (int s = 0; s < 5 && !ret; s++) {
     const CodecOp op = g2[s] ? CodecOp::G2Decompress : CodecOp::G1Decompress;
     const uint64_t rin = in_record(op), rout = out_record(op);
-    sec[s].resize(cnt[s] * rout);
     const uint32_t fl = checked[s] ? 0u : KZGPOT_NO_SUBGROUP_CHECK;
     // contiguous shards, one host thread per GPU
     std::vector<int> rc(n_gpus, 0);
@@ -213,7 +289,7 @@ int kzgpot_preprocess_buffer(const uint8_t* tr, size_t len, uint8_t* out, int mo
     for (int g = 0; g < n_gpus; g++) {
       const uint64_t lo = std::min(cnt[s], g * per), hi = std::min(cnt[s], lo + per);
       th.emplace_back([&, g, lo, hi] {
-        rc[g] = run_host(g, op, p + lo * rin, hi - lo, sec[s].data() + lo * rout, fl, &fb[g], nullptr);
+        rc[g] = run_host(g, op, p + lo * rin, hi - lo, dst[s] + lo * rout, fl, &fb[g], nullptr);
         if (fb[g] >= 0) fb[g] += (int64_t)lo;
       });
     }
@@ -225,30 +301,61 @@ int kzgpot_preprocess_buffer(const uint8_t* tr, size_t len, uint8_t* out, int mo
         if (bad_index) *bad_index = fb[g];
       }
     p += cnt[s] * rin;
+    if (!ret && out_hash && s == 0) out_hash->push(out, off_gamma);
+    if (!ret && out_hash && s == 2) out_hash->push(out + off_gamma, n * 96);
   }
-  if (ret) return ret;
-  uint8_t* o = out;
-  auto put = [&](const uint8_t* src, size_t bytes) {
-    memcpy(o, src, bytes);
-    o += bytes;
-  };
-  put(sec[0].data(), sec[0].size());  // powers_of_g = τG1
-  put(sec[2].data(), sec[2].size());  // powers_of_gamma_g = ατG1 (BTreeMap key order in fastkgz)
-  if (mode == KZGPOT_MODE_KZG) {      // VerifierKey{g, gamma_g, h, beta_h} (preprocess-kgz.rs:177-194)
-    put(sec[0].data(), 96);
-    put(sec[2].data(), 96);
-    put(sec[1].data(), 192);
-    put(sec[1].data() + 192, 192);
-  } else {                            // h, beta_h, neg_powers_of_h (empty), powers_of_h (fkgz:200-208)
-    put(sec[1].data(), 192);
-    put(sec[1].data() + 192, 192);
-    put(sec[1].data(), sec[1].size());
+  if (!ret) {
+    uint8_t* o = out + off_tail;
+    const uint8_t* tau_g2 = mode == KZGPOT_MODE_FASTKZG ? dst[1] : scratch[1].data();
+    if (mode == KZGPOT_MODE_KZG) {  // VerifierKey{g, gamma_g, h, beta_h} (preprocess-kgz.rs:177-194)
+      memcpy(o, out, 96);
+      memcpy(o + 96, out + off_gamma, 96);
+      memcpy(o + 192, tau_g2, 384);
+      if (out_hash) out_hash->push(o, 576);
+    } else {  // h, beta_h, neg_powers_of_h (empty), powers_of_h (preprocess-fastkgz.rs:200-208)
+      memcpy(o, tau_g2, 384);
+      if (out_hash) out_hash->push(o, 384 + n * 192);
+    }
   }
+  if (out_hash) {
+    uint8_t d[64];
+    out_hash->finish(d);
+    if (!ret) to_hex(d, out_hex);
+  }
+  if (want_in) {
+    in_hash.join();
+    char hex[129];
+    to_hex(in_digest, hex);
+    if (in_hex) memcpy(in_hex, hex, 129);
+    if (!ret && expect_in_hex && strncmp(hex, expect_in_hex, 128) != 0) ret = KZGPOT_E_DIGEST;
+  }
+  return ret;
+}
+
+}  // namespace
+
+extern "C" {
+
+int kzgpot_blake2b(const uint8_t* data, size_t len, uint8_t* digest64) {
+  if ((!data && len) || !digest64) return KZGPOT_E_INVALID_ARG;
+  blake2b_512(data, len, digest64);
   return 0;
 }
 
-int kzgpot_preprocess(const char* transcript_path, const char* out_path, int mode, uint32_t n_log2, int n_gpus,
-                      int* bad_section, int64_t* bad_index) {
+int kzgpot_preprocess_buffer_ex(const uint8_t* tr, size_t len, uint8_t* out, int mode, uint32_t n_log2,
+                                int n_gpus, const char* expect_transcript_digest, char* transcript_digest,
+                                char* output_digest, int* bad_section, int64_t* bad_index) {
+  return preprocess_impl(tr, len, out, mode, n_log2, n_gpus, expect_transcript_digest, transcript_digest,
+                         output_digest, bad_section, bad_index);
+}
+int kzgpot_preprocess_buffer(const uint8_t* tr, size_t len, uint8_t* out, int mode, uint32_t n_log2, int n_gpus,
+                             int* bad_section, int64_t* bad_index) {
+  return preprocess_impl(tr, len, out, mode, n_log2, n_gpus, nullptr, nullptr, nullptr, bad_section, bad_index);
+}
+
+int kzgpot_preprocess_ex(const char* transcript_path, const char* out_path, int mode, uint32_t n_log2, int n_gpus,
+                         const char* expect_transcript_digest, char* transcript_digest, char* output_digest,
+                         int* bad_section, int64_t* bad_index) {
   if (!transcript_path || !out_path) return KZGPOT_E_INVALID_ARG;
   FILE* f = fopen(transcript_path, "rb");
   if (!f) return KZGPOT_E_IO;
@@ -264,14 +371,19 @@ int kzgpot_preprocess(const char* transcript_path, const char* out_path, int mod
   fclose(f);
   if (got != tr.size()) return KZGPOT_E_IO;
   std::vector<uint8_t> out(kzgpot_output_size(n_log2, mode));
-  const int r = kzgpot_preprocess_buffer(tr.data(), tr.size(), out.data(), mode, n_log2, n_gpus, bad_section,
-                                         bad_index);
+  const int r = preprocess_impl(tr.data(), tr.size(), out.data(), mode, n_log2, n_gpus, expect_transcript_digest,
+                                transcript_digest, output_digest, bad_section, bad_index);
   if (r) return r;
   FILE* o = fopen(out_path, "wb");
   if (!o) return KZGPOT_E_IO;
   const size_t put = fwrite(out.data(), 1, out.size(), o);
   const int cr = fclose(o);
   return (put == out.size() && cr == 0) ? 0 : KZGPOT_E_IO;
+}
+int kzgpot_preprocess(const char* transcript_path, const char* out_path, int mode, uint32_t n_log2, int n_gpus,
+                      int* bad_section, int64_t* bad_index) {
+  return kzgpot_preprocess_ex(transcript_path, out_path, mode, n_log2, n_gpus, nullptr, nullptr, nullptr,
+                              bad_section, bad_index);
 }
 
 // ------------------------------------------------------------------------------- loader mirror

@@ -17,7 +17,6 @@ and panics on the first bad point — preprocess-kgz.rs:110,142).
 from __future__ import annotations
 
 import ctypes
-import hashlib
 import os
 from dataclasses import dataclass
 
@@ -151,35 +150,58 @@ def output_size(n_log2: int = TAU_POWERS_LOG2, mode: int = MODE_KZG) -> int:
     return _lib.load().kzgpot_output_size(n_log2, mode)
 
 
-def preprocess_buffer(transcript, n_log2: int, mode: int = MODE_KZG, n_gpus: int = 0) -> bytes:
-    """preprocess-{kgz,fastkgz} main on an in-memory response transcript → output file bytes."""
+@dataclass
+class PreprocessResult:
+    out: bytes | None
+    transcript_digest: str
+    output_digest: str
+
+
+def preprocess_buffer(transcript, n_log2: int, mode: int = MODE_KZG, n_gpus: int = 0,
+                      expect_transcript_digest: str | None = None, with_digests: bool = False):
+    """preprocess-{kgz,fastkgz} main on an in-memory response transcript → output file bytes
+    (or a PreprocessResult with the BLAKE2b-512 digests, computed beside the GPU pass)."""
     ptr, nbytes, keep = _buf(transcript)
     out = ctypes.create_string_buffer(output_size(n_log2, mode))
     sec, idx = ctypes.c_int(-1), ctypes.c_int64(-1)
-    r = _lib.load().kzgpot_preprocess_buffer(ptr, nbytes, out, mode, n_log2, n_gpus, ctypes.byref(sec),
-                                             ctypes.byref(idx))
+    din, dout = ctypes.create_string_buffer(129), ctypes.create_string_buffer(129)
+    exp = expect_transcript_digest.encode() if expect_transcript_digest else None
+    r = _lib.load().kzgpot_preprocess_buffer_ex(ptr, nbytes, out, mode, n_log2, n_gpus, exp,
+                                                din if (with_digests or exp) else None,
+                                                dout if with_digests else None, ctypes.byref(sec),
+                                                ctypes.byref(idx))
     del keep
     if r:
         raise KzgPotError(r, idx.value, sec.value)
+    if with_digests:
+        return PreprocessResult(out.raw, din.value.decode(), dout.value.decode())
     return out.raw
 
 
 def preprocess(transcript_path: str, out_path: str = KZG_SETUP_FILE, mode: int = MODE_KZG,
-               n_log2: int = TAU_POWERS_LOG2, n_gpus: int = 0) -> None:
-    """`preprocess-kgz` / `preprocess-fastkgz` without the download step (no network here)."""
+               n_log2: int = TAU_POWERS_LOG2, n_gpus: int = 0, check_digest: bool | None = None) -> PreprocessResult:
+    """`preprocess-kgz` / `preprocess-fastkgz` main (preprocess-kgz.rs:162-199) without the network:
+    download_parameters' transcript check (BLAKE2b == POWERSOFTAU_DIGEST, preprocess-kgz.rs:32-67)
+    runs when check_digest is True (default: only for the real 2^21 configuration); on a mismatch
+    the reference would re-download — here it raises KzgPotError(-104). Returns both digests."""
+    if check_digest is None:
+        check_digest = n_log2 == TAU_POWERS_LOG2
     sec, idx = ctypes.c_int(-1), ctypes.c_int64(-1)
-    r = _lib.load().kzgpot_preprocess(transcript_path.encode(), out_path.encode(), mode, n_log2, n_gpus,
-                                      ctypes.byref(sec), ctypes.byref(idx))
+    din, dout = ctypes.create_string_buffer(129), ctypes.create_string_buffer(129)
+    exp = POWERSOFTAU_DIGEST.encode() if check_digest else None
+    r = _lib.load().kzgpot_preprocess_ex(transcript_path.encode(), out_path.encode(), mode, n_log2, n_gpus, exp,
+                                         din, dout, ctypes.byref(sec), ctypes.byref(idx))
     if r:
         raise KzgPotError(r, idx.value, sec.value)
+    return PreprocessResult(None, din.value.decode(), dout.value.decode())
 
 
-def preprocess_kgz(transcript_path: str = "powersoftau", out_path: str = KZG_SETUP_FILE, **kw) -> None:
-    preprocess(transcript_path, out_path, MODE_KZG, **kw)
+def preprocess_kgz(transcript_path: str = "powersoftau", out_path: str = KZG_SETUP_FILE, **kw) -> PreprocessResult:
+    return preprocess(transcript_path, out_path, MODE_KZG, **kw)
 
 
-def preprocess_fastkgz(transcript_path: str = "powersoftau", out_path: str = KZG_SETUP_FILE, **kw) -> None:
-    preprocess(transcript_path, out_path, MODE_FASTKZG, **kw)
+def preprocess_fastkgz(transcript_path: str = "powersoftau", out_path: str = KZG_SETUP_FILE, **kw) -> PreprocessResult:
+    return preprocess(transcript_path, out_path, MODE_FASTKZG, **kw)
 
 
 # ------------------------------------------------------------------ loader mirror (src/lib.rs:174-228)
@@ -295,9 +317,16 @@ def load_fastkzg_setup(path: str = KZG_SETUP_FILE, n_log2: int = TAU_POWERS_LOG2
         return load_fastkzg_setup_buffer(f.read(), n_log2)
 
 
-def blake2b_hex(data: bytes) -> str:
-    """blake2b_simd::State::new().update(data).finalize().to_hex() (src/lib.rs:129)."""
-    return hashlib.blake2b(data).hexdigest()
+def blake2b_hex(data) -> str:
+    """blake2b_simd::State::new().update(data).finalize().to_hex() (src/lib.rs:129), computed by
+    the library's host BLAKE2b (the one kzgpot_preprocess_ex runs beside the GPU)."""
+    ptr, nbytes, keep = _buf(data)
+    d = ctypes.create_string_buffer(64)
+    r = _lib.load().kzgpot_blake2b(ptr, nbytes, d)
+    del keep
+    if r:
+        raise KzgPotError(r)
+    return d.raw.hex()
 
 
 def _download_setup(file_digest: str, check_digest: bool, path: str = KZG_SETUP_FILE) -> None:

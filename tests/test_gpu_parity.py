@@ -220,3 +220,24 @@ def test_load_dev_api(gpu):
     first = next(i for i, v in enumerate(vecs) if v["status"])
     assert device.read_key(key) == (first << 8) | vecs[first]["status"]
     assert d_out.cpu().numpy().tobytes() == b"".join(bytes.fromhex(v["out"]) if v["out"] else bytes(104) for v in vecs)
+
+
+def test_preprocess_digests(gpu, tmp_path):
+    """kzgpot_preprocess_ex: BLAKE2b of transcript and output computed beside the GPU pass."""
+    meta = json.load(open(os.path.join(GOLDEN, "transcript_n1024.json")))
+    src = os.path.join(GOLDEN, "transcript_n1024.bin")
+    tr = open(src, "rb").read()
+    for mode, key in ((gpu.MODE_KZG, "kgz_blake2b"), (gpu.MODE_FASTKZG, "fastkgz_blake2b")):
+        res = gpu.preprocess_buffer(tr, 10, mode, with_digests=True)
+        assert res.transcript_digest == meta["transcript_blake2b"]
+        assert res.output_digest == meta[key] == hashlib.blake2b(res.out).hexdigest()
+    out = gpu.preprocess_buffer(tr, 10, expect_transcript_digest=meta["transcript_blake2b"])
+    assert hashlib.blake2b(out).hexdigest() == meta["kgz_blake2b"]
+    with pytest.raises(gpu.KzgPotError) as e:
+        gpu.preprocess_buffer(tr, 10, expect_transcript_digest=gpu.POWERSOFTAU_DIGEST)
+    assert e.value.code == -104
+    res = gpu.preprocess_fastkgz(src, str(tmp_path / "fast"), n_log2=10)
+    assert res.output_digest == meta["fastkgz_blake2b"] and res.transcript_digest == meta["transcript_blake2b"]
+    with pytest.raises(gpu.KzgPotError) as e:
+        gpu.preprocess_kgz(src, str(tmp_path / "kgz"), n_log2=10, check_digest=True)
+    assert e.value.code == -104 and not (tmp_path / "kgz").exists()

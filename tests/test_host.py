@@ -78,3 +78,24 @@ def test_download_stub_has_no_network(kzgpot_mod, tmp_path):
     with pytest.raises(k.KzgPotError) as e:
         k.download_kzg_setup(True, path=str(p))
     assert e.value.code == -104
+
+
+def test_blake2b_matches_hashlib(kzgpot_mod):
+    """The library's host BLAKE2b-512 (used by kzgpot_preprocess_ex beside the GPU pass) against
+    hashlib, across block-boundary lengths. Host-only: no GPU needed."""
+    import hashlib
+    import random
+
+    rng = random.Random(7)
+    for n in (0, 1, 63, 64, 127, 128, 129, 255, 256, 257, 1023, 4096, 100_003):
+        data = bytes(rng.randrange(256) for _ in range(n))
+        assert kzgpot_mod.blake2b_hex(data) == hashlib.blake2b(data).hexdigest(), n
+
+
+def test_python_mirror_api_surface(kzgpot_mod):
+    """The crate's public API (src/lib.rs) and the two binaries' mains, by their reference names."""
+    for name in ("read_g1", "read_g2", "load_kzg_setup", "load_fastkzg_setup", "download_kzg_setup",
+                 "download_fastkzg_setup", "preprocess_kgz", "preprocess_fastkgz", "deserialize_unchecked",
+                 "g1_decompress", "g2_decompress", "blake2b_hex", "KZG_SETUP_FILE", "KZG_SETUP_FILE_DIGEST",
+                 "FASTKZG_SETUP_FILE_DIGEST", "POWERSOFTAU_DIGEST", "TAU_POWERS_LENGTH"):
+        assert hasattr(kzgpot_mod, name), name
