@@ -49,7 +49,8 @@ def parse():
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-log2", type=int, default=15)
-    ap.add_argument("--no-next-rows", action="store_true", help="skip the loader (SURVEY 8f) measurement")
+    ap.add_argument("--no-next-rows", action="store_true", help="skip the loader / BN254 (SURVEY 8f) measurements")
+    ap.add_argument("--bn254-log2", type=int, default=28, help="config 5 size (0 = skip)")
     return ap.parse_args()
 
 
@@ -207,6 +208,32 @@ def main():
             "achieved_GBs": load_gbs, "peak_GBs": HBM_PEAK_GBS, "hbm_frac": load_gbs / HBM_PEAK_GBS,
             "all_accepted": D.read_key(keyl) == KD.NO_BAD}}
         del outl
+        # BN254 G1, ark compressed (32 B) -> uncompressed (64 B)
+        if args.bn254_log2 > 0:
+            nb = 1 << args.bn254_log2
+            t_bn = time.perf_counter()
+            compb, expb = D.synth("bn254", args.seed + 2, 0, nb, dev, with_expected=True)
+            torch.cuda.synchronize()
+            t_bn = time.perf_counter() - t_bn
+            outb = torch.empty(nb * 64, dtype=torch.uint8, device=dev)
+            keyb = torch.empty(1, dtype=torch.int64, device=dev)
+            D.codec_dev("bn254_g1_decompress", compb, outb, keyb)  # warm-up, verified below
+            be = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            be[0].record()
+            for _ in range(3):
+                D.codec_dev("bn254_g1_decompress", compb, outb, keyb)
+            be[1].record()
+            torch.cuda.synchronize()
+            bn_ms = be[0].elapsed_time(be[1]) / 3
+            ok = D.read_key(keyb) == KD.NO_BAD and torch.equal(outb, expb)
+            next_rows["bn254_g1_decompress"] = {
+                "workload": f"config 5: 2^{args.bn254_log2} BN254 G1, ark compressed 32 B -> ark uncompressed 64 B",
+                "kernel": "k_bn254_g1_decompress", "points": nb, "launch_ms": bn_ms,
+                "points_per_s": nb / (bn_ms * 1e-3), "algorithmic_bytes_per_point": 96,
+                "achieved_GBs": 96 * nb / (bn_ms * 1e-3) / 1e9, "peak_GBs": HBM_PEAK_GBS,
+                "hbm_frac": 96 * nb / (bn_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                "verified_bit_exact": bool(ok), "generate_s": t_bn}
+            del compb, expb, outb
 
     g1_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / len(ev)
     g2_ms = sum(e[1].elapsed_time(e[2]) for e in ev) / len(ev)

@@ -164,6 +164,16 @@ int kzgpot_load_fastkzg_setup_buffer(const uint8_t* file, size_t len, uint32_t n
                                      uint8_t* powers_of_gamma_g, uint8_t* h_beta_h, uint8_t* powers_of_h,
                                      int* bad_section, int64_t* bad_index);
 
+/* ---------------------------------------------------------------- BN254 (config 5, next-row §8f 4) */
+/* No reference counterpart: the same path instantiated for ark-bn254 0.2 G1 (cofactor 1).
+ * ark compressed (32 B: x LE, SWFlags bit7 PositiveY / bit6 Infinity in byte 31) → ark
+ * uncompressed (64 B) = ark-ec 0.2 GroupAffine::deserialize + serialize_uncompressed. The point
+ * at infinity is legal (→ ark zero()). Statuses: 3 NotInField, 4 NotOnCurve, 6 UnexpectedFlags. */
+int kzgpot_bn254_g1_decompress(const uint8_t* in, size_t n, uint8_t* out, int64_t* first_bad);
+int kzgpot_bn254_g1_decompress_ex(const uint8_t* in, size_t n, uint8_t* out, int64_t* first_bad, uint8_t* status);
+int kzgpot_bn254_g1_decompress_dev(const void* d_in, size_t n, void* d_out, uint64_t* d_bad_key, uint8_t* d_status,
+                                   void* stream);
+
 /* ---------------------------------------------------------------- misc */
 const char* kzgpot_status_name(int status);  /* name of a KZGPOT_ST_* or KZGPOT_E_* code */
 int kzgpot_device_count(void);               /* visible HIP devices (0 if none) */

@@ -405,6 +405,16 @@ int kzgpot_g1_deserialize_unchecked_dev(const void* d_in, size_t n, void* d_out,
                                         uint8_t* d_status, void* stream) {
   return run_dev(CodecOp::G1Load, d_in, n, d_out, 0, d_bad_key, d_status, stream);
 }
+int kzgpot_bn254_g1_decompress_ex(const uint8_t* in, size_t n, uint8_t* out, int64_t* first_bad, uint8_t* status) {
+  return run_host(current_device(), CodecOp::Bn254G1Decompress, in, n, out, 0, first_bad, status);
+}
+int kzgpot_bn254_g1_decompress(const uint8_t* in, size_t n, uint8_t* out, int64_t* first_bad) {
+  return kzgpot_bn254_g1_decompress_ex(in, n, out, first_bad, nullptr);
+}
+int kzgpot_bn254_g1_decompress_dev(const void* d_in, size_t n, void* d_out, uint64_t* d_bad_key, uint8_t* d_status,
+                                   void* stream) {
+  return run_dev(CodecOp::Bn254G1Decompress, d_in, n, d_out, 0, d_bad_key, d_status, stream);
+}
 int kzgpot_g2_deserialize_unchecked_dev(const void* d_in, size_t n, void* d_out, uint64_t* d_bad_key,
                                         uint8_t* d_status, void* stream) {
   return run_dev(CodecOp::G2Load, d_in, n, d_out, 0, d_bad_key, d_status, stream);

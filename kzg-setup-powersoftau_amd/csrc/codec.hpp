@@ -9,7 +9,7 @@ namespace kzgpot {
 
 constexpr int kBlock = 256;  // 4 waves; one point per lane
 
-enum class CodecOp { G1Decompress, G2Decompress, G1Transcode, G2Transcode, G1Load, G2Load };
+enum class CodecOp { G1Decompress, G2Decompress, G1Transcode, G2Transcode, G1Load, G2Load, Bn254G1Decompress };
 
 // record sizes on the wire
 constexpr uint64_t in_record(CodecOp op) {
@@ -20,6 +20,7 @@ constexpr uint64_t in_record(CodecOp op) {
     case CodecOp::G2Transcode: return 192;
     case CodecOp::G1Load: return 96;
     case CodecOp::G2Load: return 192;
+    case CodecOp::Bn254G1Decompress: return 32;
   }
   return 0;
 }
@@ -31,6 +32,7 @@ constexpr uint64_t out_record(CodecOp op) {
     case CodecOp::G2Transcode: return 192;
     case CodecOp::G1Load: return KZGPOT_G1_ARK_MONT_BYTES;
     case CodecOp::G2Load: return KZGPOT_G2_ARK_MONT_BYTES;
+    case CodecOp::Bn254G1Decompress: return 64;
   }
   return 0;
 }
@@ -38,6 +40,10 @@ constexpr uint64_t out_record(CodecOp op) {
 // loader kernels (load_kernels.hip)
 hipError_t launch_load(bool g2, const void* d_in, void* d_out, uint64_t n, unsigned long long* d_first_bad,
                        uint8_t* d_status, hipStream_t stream);
+
+// BN254 G1 codec (bn254_kernels.hip)
+hipError_t launch_bn254(const void* d_in, void* d_out, uint64_t n, unsigned long long* d_first_bad,
+                        uint8_t* d_status, hipStream_t stream);
 
 hipError_t launch_codec(CodecOp op, const void* d_in, void* d_out, uint64_t n, uint32_t flags,
                         unsigned long long* d_first_bad, uint8_t* d_status, hipStream_t stream);

@@ -435,6 +435,8 @@ hipError_t launch_codec(CodecOp op, const void* d_in, void* d_out, uint64_t n, u
     case CodecOp::G1Load:
     case CodecOp::G2Load:
       return launch_load(op == CodecOp::G2Load, d_in, d_out, n, d_first_bad, d_status, stream);
+    case CodecOp::Bn254G1Decompress:
+      return launch_bn254(d_in, d_out, n, d_first_bad, d_status, stream);
   }
   return hipGetLastError();
 }

@@ -70,12 +70,12 @@ KZG_DEV void jac_dbl(jac<fp>& p) {
   fp_mul(p.z, t, p.z);         // Z3 = 2 Y Z                 N
   fp_sqr(a, e);                // F = E^2                    N
   fp_shl_nr<1>(t, d);          // 2D                        < 2^29
-  fp_subk_nr(p.x, a, t, KB_8_29);  // X3 = F - 2D           < 2^30 + 2^28
+  fp_subk_nr(p.x, a, t, BlsFp::KB_8_29);  // X3 = F - 2D           < 2^30 + 2^28
   fp_mul3_nr(t, d);            // 3D
-  fp_subk_nr(t, t, a, KB_8_28);    // D - X3 = 3D - F       < 5 * 2^28
+  fp_subk_nr(t, t, a, BlsFp::KB_8_28);    // D - X3 = 3D - F       < 5 * 2^28
   fp_mul(t, e, t);             // E (D - X3)                 N
   fp_shl_nr<1>(c8, c8);        // 8C                        < 2^29
-  fp_subk_nr(p.y, t, c8, KB_8_29); // Y3 = E (D - X3) - 8C  < 2^30
+  fp_subk_nr(p.y, t, c8, BlsFp::KB_8_29); // Y3 = E (D - X3) - 8C  < 2^30
 }
 
 // Generic (Fp2, cold): all values reduced (< 2p) through the Fp2 helpers above.
@@ -97,13 +97,13 @@ KZG_DEV void jac_dbl(jac<F>& p) {
   f_mul(p.z, t, p.z);          // Z3 = 2YZ
   f_sqr(a, e);                 // F
   f_shl<1>(t, d);
-  f_subk(p.x, a, t, KB_64_29);
+  f_subk(p.x, a, t, BlsFp::KB_64_29);
   f_norm(p.x, p.x);            // X3 = F - 2D
   f_mul3(t, d);
-  f_subk(t, t, a, KB_16_28);
+  f_subk(t, t, a, BlsFp::KB_16_28);
   f_norm(t, t);                // 3D - F
   f_mul(t, e, t);
-  f_subk(p.y, t, c8, KB_32_28);
+  f_subk(p.y, t, c8, BlsFp::KB_32_28);
   f_norm(p.y, p.y);            // Y3
 }
 
@@ -115,11 +115,11 @@ KZG_DEV void jac_madd(jac<F>& p, const F& x2, const F& y2) {
   F z1z1, h, r, t;
   f_sqr(z1z1, p.z);
   f_mul(h, x2, z1z1);          // U2
-  f_subk(h, h, p.x, KB_128_31);
+  f_subk(h, h, p.x, BlsFp::KB_128_31);
   f_norm(h, h);                // H = U2 - X1
   f_mul(t, y2, p.z);
   f_mul(t, t, z1z1);           // S2
-  f_subk(r, t, p.y, KB_64_31);
+  f_subk(r, t, p.y, BlsFp::KB_64_31);
   f_norm(r, r);                // r' = S2 - Y1   (ark's r = 2 r')
   const bool z1zero = f_is_zero(p.z);
   const bool same = !z1zero && f_is_zero(h) && f_is_zero(r);
@@ -144,11 +144,11 @@ KZG_DEV void jac_madd(jac<F>& p, const F& x2, const F& y2) {
   f_mul(hh, p.x, hh);          // V = X1 I
   f_sqr(t, r);                 // r'^2
   f_shl<2>(t, t);              // r^2 = 4 r'^2
-  f_subk(t, t, j, KB_32_28);
+  f_subk(t, t, j, BlsFp::KB_32_28);
   f_shl<1>(h, hh);             // 2V
-  f_subk(t, t, h, KB_64_29);
+  f_subk(t, t, h, BlsFp::KB_64_29);
   f_norm(t, t);                // X3 = r^2 - J - 2V
-  f_subk(hh, hh, t, KB_128_28);
+  f_subk(hh, hh, t, BlsFp::KB_128_28);
   f_norm(hh, hh);              // V - X3
   f_shl<1>(r, r);
   f_norm(r, r);                // r = 2 r'
@@ -156,7 +156,7 @@ KZG_DEV void jac_madd(jac<F>& p, const F& x2, const F& y2) {
   f_shl<1>(h, p.y);
   f_norm(h, h);
   f_mul(j, h, j);              // 2 Y1 J
-  f_subk(p.y, hh, j, KB_32_28);
+  f_subk(p.y, hh, j, BlsFp::KB_32_28);
   f_norm(p.y, p.y);            // Y3
   p.x = t;
 }
@@ -174,11 +174,11 @@ KZG_DEV void jac_add(jac<F>& p, const jac<F>& q) {
   f_mul(s1, p.y, q.z);
   f_mul(s1, s1, z2z2);         // S1
   f_mul(h, q.x, z1z1);
-  f_subk(h, h, u1, KB_8_28);
+  f_subk(h, h, u1, BlsFp::KB_8_28);
   f_norm(h, h);                // H = U2 - U1
   f_mul(r, q.y, p.z);
   f_mul(r, r, z1z1);
-  f_subk(r, r, s1, KB_8_28);
+  f_subk(r, r, s1, BlsFp::KB_8_28);
   f_norm(r, r);                // r' = S2 - S1
   const bool same = !pzero && !qzero && f_is_zero(h) && f_is_zero(r);
   if (__builtin_expect(pzero || qzero || same, 0)) {
@@ -199,11 +199,11 @@ KZG_DEV void jac_add(jac<F>& p, const jac<F>& q) {
   f_mul(u1, u1, z1z1);         // V = U1 I
   f_sqr(h, r);
   f_shl<2>(h, h);              // r^2 = 4 r'^2
-  f_subk(h, h, z2z2, KB_8_28);
+  f_subk(h, h, z2z2, BlsFp::KB_8_28);
   f_shl<1>(z1z1, u1);
-  f_subk(h, h, z1z1, KB_64_29);
+  f_subk(h, h, z1z1, BlsFp::KB_64_29);
   f_norm(h, h);                // X3 = r^2 - J - 2V
-  f_subk(u1, u1, h, KB_128_28);
+  f_subk(u1, u1, h, BlsFp::KB_128_28);
   f_norm(u1, u1);              // V - X3
   f_shl<1>(r, r);
   f_norm(r, r);
@@ -211,7 +211,7 @@ KZG_DEV void jac_add(jac<F>& p, const jac<F>& q) {
   f_shl<1>(s1, s1);
   f_norm(s1, s1);
   f_mul(s1, s1, z2z2);         // 2 S1 J
-  f_subk(p.y, u1, s1, KB_8_28);
+  f_subk(p.y, u1, s1, BlsFp::KB_8_28);
   f_norm(p.y, p.y);            // Y3
   p.x = h;
 }
@@ -248,11 +248,11 @@ KZG_DEV bool jac_eq_affine(const jac<F>& p, const F& x, const F& y) {
   F z2, t;
   f_sqr(z2, p.z);
   f_mul(t, x, z2);
-  f_subk(t, t, p.x, KB_128_31);
+  f_subk(t, t, p.x, BlsFp::KB_128_31);
   bool ok = f_is_zero(t);
   f_mul(z2, z2, p.z);
   f_mul(t, y, z2);
-  f_subk(t, t, p.y, KB_128_31);
+  f_subk(t, t, p.y, BlsFp::KB_128_31);
   ok = ok && f_is_zero(t);
   return ok && !f_is_zero(p.z);
 }

@@ -1,22 +1,23 @@
-// BLS12-381 base-field arithmetic for gfx950 (CDNA4), one field element per lane.
+// Prime-field arithmetic for gfx950 (CDNA4), one field element per lane — generic over the field
+// (traits struct: BlsFp = BLS12-381 Fq, Bn254Fp = BN254 Fq; tools/gen_constants.py).
 //
-// Representation: 14 limbs of 28 bits, each held in a 32-bit VGPR, Montgomery form with
-// R = 2^392. The 4 spare bits per limb are the point of the design:
+// Representation: NL limbs of 28 bits, each held in a 32-bit VGPR, Montgomery form with
+// R = 2^(28 NL) (BLS12-381: 14 limbs, R = 2^392; BN254: 10 limbs, R = 2^280). The 4 spare bits
+// per limb are the point of the design:
 //
 //  * Multiply (fp_mul): finely-integrated product scanning where every column sum fits ONE
 //    64-bit accumulator — up to 14 products a_j b_k < 2^60 (operand limbs < 2^30 / 2^32 x 2^28)
 //    plus 14 products m_j p_k < 2^56 plus a < 2^36 carry stays below 2^63.9 — so each 32x32
 //    product is a single v_mad_u64_u32 and no carry ever passes through an SGPR. The radix-2^32
 //    alternative needs mad + addc per product and gfx950 requires wait states around SGPR carry
-//    hand-offs; measured 73.4 vs 62.2 G Fp-mul/s at 2 waves/SIMD
-//    (tools/microbench/mont28.hip, mont_variants.hip).
+//    hand-offs; measured 75.5 vs 63.7 G Fp-mul/s (tools/microbench/mont28.hip, mont_variants.hip).
 //  * Add / subtract are limb-wise and carry-free: a + b, and a - b as a + KB - b where KB is a
 //    multiple of p in a "borrowed" limb form whose every limb dominates b's (bls12_381_consts.hpp).
-//    14 VALU instructions, no carry chain, no wait states.
+//    NL VALU instructions, no carry chain, no wait states.
 //
 // Bounds discipline (checked for every formula by tests/test_field_bounds.py): a value is
 // "normalized" (N) when all limbs < 2^28; fp_mul needs limb-bit(a) + limb-bit(b) <= 60 and returns
-// N with value < p (1 + v(a) v(b) / 2^11); loose values (limbs up to 2^30-2^32 after a few
+// N with value < p (1 + v(a) v(b) p / R); loose values (limbs up to 2^30-2^32 after a few
 // limb-wise adds) only ever feed fp_mul or a further limb-wise op, never storage-to-bytes or a
 // comparison, which go through fp_norm / fp_canon.
 //
@@ -27,209 +28,232 @@
 #include <stdint.h>
 
 #include "bls12_381_consts.hpp"
+#include "bn254_consts.hpp"
 
 #define KZG_DEV __device__ __forceinline__
 
 namespace kzgpot {
 
-constexpr int NL = 14;
 constexpr uint32_t LMASK = (1u << 28) - 1;
 
-struct fp {
-  uint32_t v[NL];
+template <class Tr>
+struct Fe {
+  uint32_t v[Tr::NL];
 };
+using fp = Fe<BlsFp>;        // BLS12-381 Fq
+using fpbn = Fe<Bn254Fp>;    // BN254 Fq
+constexpr int NL = BlsFp::NL;
 
-KZG_DEV void fp_set(fp& r, const uint32_t (&c)[NL]) {
+template <class Tr>
+KZG_DEV void fp_set(Fe<Tr>& r, const uint32_t (&c)[Tr::NL]) {
 #pragma unroll
-  for (int i = 0; i < NL; i++) r.v[i] = c[i];
+  for (int i = 0; i < Tr::NL; i++) r.v[i] = c[i];
 }
-KZG_DEV void fp_zero(fp& r) {
+template <class Tr>
+KZG_DEV void fp_zero(Fe<Tr>& r) {
 #pragma unroll
-  for (int i = 0; i < NL; i++) r.v[i] = 0;
+  for (int i = 0; i < Tr::NL; i++) r.v[i] = 0;
 }
 
 // ------------------------------------------------------------------------------- multiply
 // r = a b R^-1 mod p. Requires limb-bit(a) + limb-bit(b) <= 60 (see header). Output normalized.
-KZG_DEV void fp_mul(fp& r, const fp& a, const fp& b) {
-  uint32_t m[NL];
+template <class Tr>
+KZG_DEV void fp_mul(Fe<Tr>& r, const Fe<Tr>& a, const Fe<Tr>& b) {
+  constexpr int N = Tr::NL;
+  uint32_t m[N];
   uint64_t acc = 0;
 #pragma unroll
-  for (int i = 0; i < 2 * NL; i++) {
-    const int j0 = i < NL ? 0 : i - (NL - 1);
-    const int j1 = i < NL ? i - 1 : NL - 1;
+  for (int i = 0; i < 2 * N; i++) {
+    const int j0 = i < N ? 0 : i - (N - 1);
+    const int j1 = i < N ? i - 1 : N - 1;
     uint64_t accp = 0;  // m*p terms in their own chain: two independent mad chains per column
 #pragma unroll
     for (int j = j0; j <= j1; j++) {
       acc += (uint64_t)a.v[j] * b.v[i - j];
-      accp += (uint64_t)m[j] * FP_P[i - j];
+      accp += (uint64_t)m[j] * Tr::P[i - j];
     }
-    if (i < NL) {
+    if (i < N) {
       acc += (uint64_t)a.v[i] * b.v[0];
       acc += accp;
-      m[i] = ((uint32_t)acc * FP_PINV) & LMASK;
-      acc += (uint64_t)m[i] * FP_P[0];
+      m[i] = ((uint32_t)acc * Tr::PINV) & LMASK;
+      acc += (uint64_t)m[i] * Tr::P[0];
     } else {
       acc += accp;
-      r.v[i - NL] = (uint32_t)acc & LMASK;
+      r.v[i - N] = (uint32_t)acc & LMASK;
     }
     acc >>= 28;
   }
 }
 // r = a^2 R^-1 mod p: each cross product a_j a_k (j < k) once, as a_j (2 a_k), plus the squares —
-// 105 instead of 196 products for the a*a half (the 196 m*p products of the reduction stay).
-// Every column partial sum is at most fp_mul(a, a)'s, so the same bounds hold; in addition
+// NL(NL+1)/2 instead of NL^2 products for the a*a half (the NL^2 m*p products of the reduction
+// stay). Every column partial sum is at most fp_mul(a, a)'s, so the same bounds hold; in addition
 // a's limbs must be < 2^31 so that 2 a_k fits 32 bits.
-KZG_DEV void fp_sqr(fp& r, const fp& a) {
-  uint32_t d[NL], m[NL];
+template <class Tr>
+KZG_DEV void fp_sqr(Fe<Tr>& r, const Fe<Tr>& a) {
+  constexpr int N = Tr::NL;
+  uint32_t d[N], m[N];
 #pragma unroll
-  for (int j = 0; j < NL; j++) d[j] = a.v[j] << 1;
+  for (int j = 0; j < N; j++) d[j] = a.v[j] << 1;
   uint64_t acc = 0;
 #pragma unroll
-  for (int i = 0; i < 2 * NL - 1; i++) {
-    const int j0 = i < NL ? 0 : i - (NL - 1);
+  for (int i = 0; i < 2 * N - 1; i++) {
+    const int j0 = i < N ? 0 : i - (N - 1);
     uint64_t accp = 0;
 #pragma unroll
     for (int j = j0; 2 * j < i; j++) acc += (uint64_t)a.v[j] * d[i - j];
     if ((i & 1) == 0) acc += (uint64_t)a.v[i / 2] * a.v[i / 2];
-    const int k0 = i < NL ? 0 : i - (NL - 1);
-    const int k1 = i < NL ? i - 1 : NL - 1;
+    const int k1 = i < N ? i - 1 : N - 1;
 #pragma unroll
-    for (int k = k0; k <= k1; k++) accp += (uint64_t)m[k] * FP_P[i - k];
+    for (int k = j0; k <= k1; k++) accp += (uint64_t)m[k] * Tr::P[i - k];
     acc += accp;
-    if (i < NL) {
-      m[i] = ((uint32_t)acc * FP_PINV) & LMASK;
-      acc += (uint64_t)m[i] * FP_P[0];
+    if (i < N) {
+      m[i] = ((uint32_t)acc * Tr::PINV) & LMASK;
+      acc += (uint64_t)m[i] * Tr::P[0];
     } else {
-      r.v[i - NL] = (uint32_t)acc & LMASK;
+      r.v[i - N] = (uint32_t)acc & LMASK;
     }
     acc >>= 28;
   }
-  r.v[NL - 1] = (uint32_t)acc & LMASK;  // column 2 NL - 1 holds only the carry
+  r.v[N - 1] = (uint32_t)acc & LMASK;  // column 2 NL - 1 holds only the carry
 }
 
 // ------------------------------------------------------------------------------- limb-wise ops
-KZG_DEV void fp_add_nr(fp& r, const fp& a, const fp& b) {
+template <class Tr>
+KZG_DEV void fp_add_nr(Fe<Tr>& r, const Fe<Tr>& a, const Fe<Tr>& b) {
 #pragma unroll
-  for (int i = 0; i < NL; i++) r.v[i] = a.v[i] + b.v[i];
+  for (int i = 0; i < Tr::NL; i++) r.v[i] = a.v[i] + b.v[i];
 }
-template <int S>
-KZG_DEV void fp_shl_nr(fp& r, const fp& a) {  // 2^S a, limb-wise
+template <int S, class Tr>
+KZG_DEV void fp_shl_nr(Fe<Tr>& r, const Fe<Tr>& a) {  // 2^S a, limb-wise
 #pragma unroll
-  for (int i = 0; i < NL; i++) r.v[i] = a.v[i] << S;
+  for (int i = 0; i < Tr::NL; i++) r.v[i] = a.v[i] << S;
 }
-KZG_DEV void fp_mul3_nr(fp& r, const fp& a) {
+template <class Tr>
+KZG_DEV void fp_mul3_nr(Fe<Tr>& r, const Fe<Tr>& a) {
 #pragma unroll
-  for (int i = 0; i < NL; i++) r.v[i] = (a.v[i] << 1) + a.v[i];
+  for (int i = 0; i < Tr::NL; i++) r.v[i] = (a.v[i] << 1) + a.v[i];
 }
 // r = a + K - b with K a borrowed multiple of p dominating b limb by limb
-KZG_DEV void fp_subk_nr(fp& r, const fp& a, const fp& b, const uint32_t (&k)[NL]) {
+template <class Tr>
+KZG_DEV void fp_subk_nr(Fe<Tr>& r, const Fe<Tr>& a, const Fe<Tr>& b, const uint32_t (&k)[Tr::NL]) {
 #pragma unroll
-  for (int i = 0; i < NL; i++) r.v[i] = (a.v[i] + k[i]) - b.v[i];
+  for (int i = 0; i < Tr::NL; i++) r.v[i] = (a.v[i] + k[i]) - b.v[i];
 }
 // carry-propagate to 28-bit limbs (value unchanged; top limb keeps the excess)
-KZG_DEV void fp_norm(fp& r, const fp& a) {
+template <class Tr>
+KZG_DEV void fp_norm(Fe<Tr>& r, const Fe<Tr>& a) {
   uint32_t c = 0;
 #pragma unroll
-  for (int i = 0; i < NL - 1; i++) {
+  for (int i = 0; i < Tr::NL - 1; i++) {
     const uint32_t t = a.v[i] + c;
     r.v[i] = t & LMASK;
     c = t >> 28;
   }
-  r.v[NL - 1] = a.v[NL - 1] + c;
+  r.v[Tr::NL - 1] = a.v[Tr::NL - 1] + c;
 }
-KZG_DEV void fp_select(fp& r, bool c, const fp& a, const fp& b) {  // r = c ? a : b
+template <class Tr>
+KZG_DEV void fp_select(Fe<Tr>& r, bool c, const Fe<Tr>& a, const Fe<Tr>& b) {  // r = c ? a : b
 #pragma unroll
-  for (int i = 0; i < NL; i++) r.v[i] = c ? a.v[i] : b.v[i];
+  for (int i = 0; i < Tr::NL; i++) r.v[i] = c ? a.v[i] : b.v[i];
 }
 
 // normalized a - k (k normalized constant): returns borrow (true if a < k); d = a - k if not
-KZG_DEV bool fp_sub_const_borrow(fp& d, const fp& a, const uint32_t (&k)[NL]) {
+template <class Tr>
+KZG_DEV bool fp_sub_const_borrow(Fe<Tr>& d, const Fe<Tr>& a, const uint32_t (&k)[Tr::NL]) {
   int32_t br = 0;
 #pragma unroll
-  for (int i = 0; i < NL; i++) {
+  for (int i = 0; i < Tr::NL; i++) {
     const int32_t t = (int32_t)a.v[i] - (int32_t)k[i] + br;
     d.v[i] = (uint32_t)t & LMASK;
     br = t >> 28;  // arithmetic: 0 or -1
   }
   return br != 0;
 }
+// normalized, value < 2 p -> canonical (one conditional subtraction)
+template <class Tr>
+KZG_DEV void fp_reduce_once(Fe<Tr>& r, const Fe<Tr>& a) {
+  Fe<Tr> d;
+  const bool b = fp_sub_const_borrow(d, a, Tr::P);
+  fp_select(r, b, a, d);
+}
 // normalized, value < 256 p  ->  canonical (normalized, value in [0, p))
-KZG_DEV void fp_reduce_canon(fp& r, const fp& a) {
-  fp x = a, d;
+template <class Tr>
+KZG_DEV void fp_reduce_canon(Fe<Tr>& r, const Fe<Tr>& a) {
+  Fe<Tr> x = a, d;
 #define KZG_RED_STEP(K)                          \
   {                                              \
     const bool b = fp_sub_const_borrow(d, x, K); \
     fp_select(x, b, x, d);                       \
   }
-  KZG_RED_STEP(FP_P_X128)
-  KZG_RED_STEP(FP_P_X64)
-  KZG_RED_STEP(FP_P_X32)
-  KZG_RED_STEP(FP_P_X16)
-  KZG_RED_STEP(FP_P_X8)
-  KZG_RED_STEP(FP_P_X4)
-  KZG_RED_STEP(FP_P_X2)
-  KZG_RED_STEP(FP_P_X1)
+  KZG_RED_STEP(Tr::P_X128)
+  KZG_RED_STEP(Tr::P_X64)
+  KZG_RED_STEP(Tr::P_X32)
+  KZG_RED_STEP(Tr::P_X16)
+  KZG_RED_STEP(Tr::P_X8)
+  KZG_RED_STEP(Tr::P_X4)
+  KZG_RED_STEP(Tr::P_X2)
+  KZG_RED_STEP(Tr::P_X1)
 #undef KZG_RED_STEP
   r = x;
 }
-// normalized, value < 2 p -> canonical (one conditional subtraction)
-KZG_DEV void fp_reduce_once(fp& r, const fp& a) {
-  fp d;
-  const bool b = fp_sub_const_borrow(d, a, FP_P);
-  fp_select(r, b, a, d);
-}
 // any value with limbs < 2^32 - 16 and value < 256 p -> canonical
-KZG_DEV void fp_canon(fp& r, const fp& a) {
-  fp n;
+template <class Tr>
+KZG_DEV void fp_canon(Fe<Tr>& r, const Fe<Tr>& a) {
+  Fe<Tr> n;
   fp_norm(n, a);
   fp_reduce_canon(r, n);
 }
-KZG_DEV bool fp_is_zero_canon(const fp& c) {
+template <class Tr>
+KZG_DEV bool fp_is_zero_canon(const Fe<Tr>& c) {
   uint32_t o = 0;
 #pragma unroll
-  for (int i = 0; i < NL; i++) o |= c.v[i];
+  for (int i = 0; i < Tr::NL; i++) o |= c.v[i];
   return o == 0;
 }
-KZG_DEV bool fp_is_zero(const fp& a) {
-  fp c;
+template <class Tr>
+KZG_DEV bool fp_is_zero(const Fe<Tr>& a) {
+  Fe<Tr> c;
   fp_canon(c, a);
   return fp_is_zero_canon(c);
 }
-// a == b (mod p) for b normalized with value < 63 p (KB_64_31 dominates limbs < 2^31 - 8)
-KZG_DEV bool fp_eq(const fp& a, const fp& b) {
-  fp d;
-  fp_subk_nr(d, a, b, KB_64_31);
+// a == b (mod p) for b dominated by Tr::KB_EQ (BLS: limbs < 2^31 - 8, value < 63 p;
+// BN254: normalized, value < 4 p)
+template <class Tr>
+KZG_DEV bool fp_eq(const Fe<Tr>& a, const Fe<Tr>& b) {
+  Fe<Tr> d;
+  fp_subk_nr(d, a, b, Tr::KB_EQ);
   return fp_is_zero(d);
 }
 // canonical a < canonical b
-KZG_DEV bool fp_lt_canon(const fp& a, const fp& b) {
-  fp d;
+template <class Tr>
+KZG_DEV bool fp_lt_canon(const Fe<Tr>& a, const Fe<Tr>& b) {
+  Fe<Tr> d;
   return fp_sub_const_borrow(d, a, b.v);
 }
 // canonical p - c, with p - 0 mapped to 0
-KZG_DEV void fp_neg_canon(fp& r, const fp& c) {
-  fp pp;
-  fp_set(pp, FP_P);
+template <class Tr>
+KZG_DEV void fp_neg_canon(Fe<Tr>& r, const Fe<Tr>& c) {
   int32_t br = 0;
   const bool z = fp_is_zero_canon(c);
 #pragma unroll
-  for (int i = 0; i < NL; i++) {
-    const int32_t t = (int32_t)pp.v[i] - (int32_t)c.v[i] + br;
+  for (int i = 0; i < Tr::NL; i++) {
+    const int32_t t = (int32_t)Tr::P[i] - (int32_t)c.v[i] + br;
     r.v[i] = z ? 0u : ((uint32_t)t & LMASK);
     br = t >> 28;
   }
 }
 
 // "safe" ops for the cold paths: results normalized
-KZG_DEV void fp_add(fp& r, const fp& a, const fp& b) {
-  fp t;
+template <class Tr>
+KZG_DEV void fp_add(Fe<Tr>& r, const Fe<Tr>& a, const Fe<Tr>& b) {
+  Fe<Tr> t;
   fp_add_nr(t, a, b);
   fp_norm(r, t);
 }
-// a - b for b with limbs < 2^31 - 8 and value < 63 p
+// a - b for b with limbs < 2^31 - 8 and value < 63 p (BLS12-381)
 KZG_DEV void fp_sub(fp& r, const fp& a, const fp& b) {
   fp t;
-  fp_subk_nr(t, a, b, KB_64_31);
+  fp_subk_nr(t, a, b, BlsFp::KB_64_31);
   fp_norm(r, t);
 }
 KZG_DEV void fp_neg(fp& r, const fp& a) {
@@ -239,42 +263,49 @@ KZG_DEV void fp_neg(fp& r, const fp& a) {
 }
 
 // ------------------------------------------------------------------------------- bytes <-> limbs
-// 12 little-endian 32-bit words (a 384-bit integer) <-> 14 x 28-bit limbs
-KZG_DEV void fp_from_words(fp& r, const uint32_t (&w)[12]) {
+// NW little-endian 32-bit words (the serialized integer) <-> NL x 28-bit limbs
+template <class Tr>
+KZG_DEV void fp_from_words(Fe<Tr>& r, const uint32_t (&w)[Tr::NW]) {
 #pragma unroll
-  for (int k = 0; k < NL; k++) {
+  for (int k = 0; k < Tr::NL; k++) {
     const int bit = 28 * k, i = bit >> 5, off = bit & 31;
-    const uint32_t lo = w[i] >> off;
-    const uint32_t hi = (off > 4 && i + 1 < 12) ? (w[i + 1] << (32 - off)) : 0u;
+    const uint32_t lo = i < Tr::NW ? w[i] >> off : 0u;
+    const uint32_t hi = (off > 4 && i + 1 < Tr::NW) ? (w[i + 1] << (32 - off)) : 0u;
     r.v[k] = (lo | hi) & LMASK;
   }
 }
-KZG_DEV void fp_to_words(uint32_t (&w)[12], const fp& c) {  // c normalized, value < 2^384
+template <class Tr>
+KZG_DEV void fp_to_words(uint32_t (&w)[Tr::NW], const Fe<Tr>& c) {  // c normalized, value < 2^(32 NW)
 #pragma unroll
-  for (int j = 0; j < 12; j++) {
+  for (int j = 0; j < Tr::NW; j++) {
     const int bit = 32 * j, k = bit / 28, off = bit % 28;
     uint32_t v = c.v[k] >> off;
-    if (k + 1 < NL) v |= c.v[k + 1] << (28 - off);
-    if (off > 24 && k + 2 < NL) v |= c.v[k + 2] << (56 - off);
+    if (k + 1 < Tr::NL) v |= c.v[k + 1] << (28 - off);
+    if (off > 24 && k + 2 < Tr::NL) v |= c.v[k + 2] << (56 - off);
     w[j] = v;
   }
 }
 // canonical word vector compared with p: true if v >= p
-KZG_DEV bool words_geq_p(const uint32_t (&v)[12]) {
+template <class Tr>
+KZG_DEV bool words_geq_p_t(const uint32_t (&v)[Tr::NW]) {
   uint32_t br = 0;
 #pragma unroll
-  for (int i = 0; i < 12; i++) (void)__builtin_subc(v[i], P_WORDS[i], br, &br);
+  for (int i = 0; i < Tr::NW; i++) (void)__builtin_subc(v[i], Tr::P_WORDS[i], br, &br);
   return br == 0;
 }
-KZG_DEV void fp_to_mont(fp& r, const fp& canon) {
-  fp r2;
-  fp_set(r2, FP_R2);
+KZG_DEV bool words_geq_p(const uint32_t (&v)[BlsFp::NW]) { return words_geq_p_t<BlsFp>(v); }
+
+template <class Tr>
+KZG_DEV void fp_to_mont(Fe<Tr>& r, const Fe<Tr>& canon) {
+  Fe<Tr> r2;
+  fp_set(r2, Tr::R2);
   fp_mul(r, canon, r2);
 }
-// Montgomery -> canonical (normalized, [0, p)). For normalized a (< 2^392 = R) the Montgomery
-// product a * 1 is (a + m p) / R < 1 + p, so one conditional subtraction finishes it.
-KZG_DEV void fp_from_mont(fp& canon, const fp& a) {
-  fp one;
+// Montgomery -> canonical (normalized, [0, p)). For normalized a (< R) the Montgomery product
+// a * 1 is (a + m p) / R < 1 + p, so one conditional subtraction finishes it.
+template <class Tr>
+KZG_DEV void fp_from_mont(Fe<Tr>& canon, const Fe<Tr>& a) {
+  Fe<Tr> one;
   fp_zero(one);
   one.v[0] = 1;
   fp_mul(canon, a, one);
@@ -283,32 +314,33 @@ KZG_DEV void fp_from_mont(fp& canon, const fp& a) {
 
 // r = a^((p-3)/4): fixed sliding-window schedule (tools/gen_constants.py), identical for every
 // lane, so the whole wave follows one instruction stream. Loops stay rolled so one square and
-// one multiply body serve all 453 operations (I-cache). Input limbs <= 2^30, output normalized.
-KZG_DEV void fp_pow_pm3d4(fp& r, const fp& a) {
-  fp tab[SQRT_TABLE];
-  fp a2;
+// one multiply body serve all operations (I-cache). Input limbs <= 2^30, output normalized.
+template <class Tr>
+KZG_DEV void fp_pow_pm3d4(Fe<Tr>& r, const Fe<Tr>& a) {
+  Fe<Tr> tab[Tr::SQRT_TABLE];
+  Fe<Tr> a2;
   fp_sqr(a2, a);
   tab[0] = a;
 #pragma clang loop unroll(full)
-  for (int k = 1; k < SQRT_TABLE; k++) fp_mul(tab[k], tab[k - 1], a2);
-  fp acc = tab[SQRT_STEP_IDX[0]];
+  for (int k = 1; k < Tr::SQRT_TABLE; k++) fp_mul(tab[k], tab[k - 1], a2);
+  Fe<Tr> acc = tab[Tr::SQRT_STEP_IDX[0]];
 #pragma unroll 1
-  for (int s = 1; s < SQRT_STEPS; s++) {
-    const int nsq = __builtin_amdgcn_readfirstlane(SQRT_STEP_SQ[s]);
-    const int idx = __builtin_amdgcn_readfirstlane(SQRT_STEP_IDX[s]);
+  for (int s = 1; s < Tr::SQRT_STEPS; s++) {
+    const int nsq = __builtin_amdgcn_readfirstlane(Tr::SQRT_STEP_SQ[s]);
+    const int idx = __builtin_amdgcn_readfirstlane(Tr::SQRT_STEP_IDX[s]);
 #pragma unroll 1
     for (int k = 0; k < nsq; k++) fp_sqr(acc, acc);
     if (idx >= 0) {
       // masked OR over the table (a select chain gets folded into a dynamically indexed
-      // load, which sends the 112-dword table to scratch)
-      fp t;
+      // load, which sends the table to scratch)
+      Fe<Tr> t;
       fp_zero(t);
 #pragma unroll
-      for (int k = 0; k < SQRT_TABLE; k++) {
+      for (int k = 0; k < Tr::SQRT_TABLE; k++) {
         uint32_t m = idx == k ? 0xffffffffu : 0u;
         asm volatile("" : "+v"(m));
 #pragma unroll
-        for (int j = 0; j < NL; j++) t.v[j] |= tab[k].v[j] & m;
+        for (int j = 0; j < Tr::NL; j++) t.v[j] |= tab[k].v[j] & m;
       }
       fp_mul(acc, acc, t);
     }
@@ -318,11 +350,11 @@ KZG_DEV void fp_pow_pm3d4(fp& r, const fp& a) {
 
 // ------------------------------------------------------------------------------- reduced ops
 // For the cold Fp2 (G2) formulas every value is kept "reduced": normalized with value < 2p.
-// Inputs of these ops must be reduced; outputs are reduced. a + b or a + 2p - b is < 4p, one
-// conditional subtraction of 2p brings it back. (fp_mul of reduced inputs is < 1.002 p: reduced.)
+// Inputs of these ops must be reduced; outputs are reduced. a + b is < 4p, one conditional
+// subtraction of 2p brings it back. (fp_mul of reduced inputs is < 1.002 p: reduced.)
 KZG_DEV void fp_cond_sub_2p(fp& r, const fp& a) {
   fp d;
-  const bool b = fp_sub_const_borrow(d, a, FP_P_X2);
+  const bool b = fp_sub_const_borrow(d, a, BlsFp::P_X2);
   fp_select(r, b, a, d);
 }
 KZG_DEV void fp_add_red(fp& r, const fp& a, const fp& b) {
@@ -345,7 +377,7 @@ KZG_DEV void fp_sub_red(fp& r, const fp& a, const fp& b) {
   uint32_t c = 0;
 #pragma unroll
   for (int i = 0; i < NL; i++) {
-    const uint32_t t = d.v[i] + FP_P_X2[i] + c;
+    const uint32_t t = d.v[i] + BlsFp::P_X2[i] + c;
     e.v[i] = t & LMASK;
     c = t >> 28;
   }
@@ -360,7 +392,7 @@ struct fp2 {
 KZG_DEV void f_mul(fp& r, const fp& a, const fp& b) { fp_mul(r, a, b); }
 KZG_DEV void f_sqr(fp& r, const fp& a) { fp_sqr(r, a); }
 KZG_DEV bool f_is_zero(const fp& a) { return fp_is_zero(a); }
-KZG_DEV void f_one(fp& r) { fp_set(r, FP_ONE); }
+KZG_DEV void f_one(fp& r) { fp_set(r, BlsFp::ONE); }
 KZG_DEV void f_norm(fp& r, const fp& a) { fp_norm(r, a); }
 
 // Karatsuba: 3 Fp multiplies; reduced in, reduced out
@@ -379,14 +411,14 @@ KZG_DEV void f_mul(fp2& r, const fp2& a, const fp2& b) {
 KZG_DEV void f_sqr(fp2& r, const fp2& a) {
   fp s, d, t;
   fp_add_nr(s, a.c0, a.c1);
-  fp_subk_nr(d, a.c0, a.c1, KB_4_28);
+  fp_subk_nr(d, a.c0, a.c1, BlsFp::KB_4_28);
   fp_shl_nr<1>(t, a.c0);
   fp_mul(r.c1, t, a.c1);
   fp_mul(r.c0, s, d);
 }
 KZG_DEV bool f_is_zero(const fp2& a) { return fp_is_zero(a.c0) && fp_is_zero(a.c1); }
 KZG_DEV void f_one(fp2& r) {
-  fp_set(r.c0, FP_ONE);
+  fp_set(r.c0, BlsFp::ONE);
   fp_zero(r.c1);
 }
 KZG_DEV void fp2_neg_red(fp2& r, const fp2& a) {

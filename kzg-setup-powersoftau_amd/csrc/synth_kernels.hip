@@ -212,6 +212,60 @@ int synth(uint64_t seed, uint64_t start, size_t n, void* d_comp, void* d_ark, vo
   return hipGetLastError() == hipSuccess ? 0 : -101;
 }
 
+// BN254 G1 (cofactor 1: every curve point is in the group): x_i = 252 random bits, then the
+// first x_i + j with x^3 + 3 a square; y or -y by a random bit; the compressed encoding sets
+// PositiveY when the chosen y > -y.
+__global__ void __launch_bounds__(kSynthBlock) k_synth_bn254(uint64_t seed, uint64_t start, uint64_t n,
+                                                             uint32_t* __restrict__ comp, uint32_t* __restrict__ ark) {
+  const uint64_t i = (uint64_t)blockIdx.x * kSynthBlock + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t gi = start + i;
+  uint32_t w[8];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const uint64_t r = splitmix64(seed ^ (0x6a09e667f3bcc909ull * (4 * gi + k + 1)));
+    w[2 * k] = (uint32_t)r;
+    w[2 * k + 1] = (uint32_t)(r >> 32);
+  }
+  w[7] &= 0x0fffffffu;  // < 2^252 < p
+  const bool flip = splitmix64(seed ^ ~gi) & 1;
+  fpbn x, y;
+  fp_from_words(x, w);
+#pragma unroll 1
+  for (int attempt = 0; attempt < 64; attempt++) {
+    fpbn xm, a, t, three;
+    fp_to_mont(xm, x);
+    fp_sqr(a, xm);
+    fp_mul(a, a, xm);
+    fp_set(three, BN_THREE);
+    fp_add(a, a, three);
+    fp_pow_pm3d4(t, a);
+    fp_mul(y, t, a);
+    fp_sqr(t, y);
+    if (fp_eq(t, a)) break;
+    x.v[0] += 1;  // x + 1 (normalize: the carry may run up the limbs)
+    fp_norm(x, x);
+  }
+  fpbn yc, nyc, ncho;
+  fp_from_mont(yc, y);
+  fp_neg_canon(nyc, yc);
+  fp_select(yc, flip, nyc, yc);  // the chosen root
+  fp_neg_canon(ncho, yc);
+  const bool positive = fp_lt_canon(ncho, yc);
+  uint32_t xw[8], yw[8];
+  fp_to_words(xw, x);
+  fp_to_words(yw, yc);
+  uint32_t* c = comp + i * 8;
+#pragma unroll
+  for (int k = 0; k < 8; k++) c[k] = xw[k];
+  if (positive) c[7] |= 0x80000000u;
+  if (ark) {
+    uint32_t* a = ark + i * 16;
+#pragma unroll
+    for (int k = 0; k < 8; k++) a[k] = xw[k], a[8 + k] = yw[k];
+  }
+}
+
 }  // namespace
 }  // namespace kzgpot
 
@@ -223,5 +277,12 @@ int kzgpot_synth_g1_dev(uint64_t seed, uint64_t start, size_t n, void* d_comp, v
 }
 int kzgpot_synth_g2_dev(uint64_t seed, uint64_t start, size_t n, void* d_comp, void* d_ark, void* stream) {
   return kzgpot::synth<kzgpot::fp2>(seed, start, n, d_comp, d_ark, stream);
+}
+// BN254 G1: ark compressed (32 B) into d_comp, expected ark uncompressed (64 B) into d_ark.
+int kzgpot_synth_bn254_dev(uint64_t seed, uint64_t start, size_t n, void* d_comp, void* d_ark, void* stream) {
+  if (n)
+    hipLaunchKernelGGL(kzgpot::k_synth_bn254, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       seed, start, (uint64_t)n, (uint32_t*)d_comp, (uint32_t*)d_ark);
+  return hipGetLastError() == hipSuccess ? 0 : -101;
 }
 }

@@ -229,6 +229,22 @@ def deserialize_unchecked(data, g2: bool = False, want_status: bool = False) -> 
     return CodecResult(out.raw[: n * rout], ret, fb.value, st.raw[:n] if st is not None else None)
 
 
+def bn254_g1_decompress(data, want_status: bool = False) -> CodecResult:
+    """BN254 G1 (config 5): ark-bn254 compressed (32 B) → ark uncompressed (64 B) on the GPU."""
+    ptr, nbytes, keep = _buf(data)
+    if nbytes % 32:
+        raise ValueError(f"bn254_g1_decompress: input length {nbytes} is not a multiple of 32")
+    n = nbytes // 32
+    out = ctypes.create_string_buffer(max(1, n * 64))
+    st = ctypes.create_string_buffer(max(1, n)) if want_status else None
+    fb = ctypes.c_int64(-1)
+    ret = _lib.load().kzgpot_bn254_g1_decompress_ex(ptr, n, out, ctypes.byref(fb), st)
+    del keep
+    if ret <= -100:
+        raise KzgPotError(ret)
+    return CodecResult(out.raw[: n * 64], ret, fb.value, st.raw[:n] if st is not None else None)
+
+
 def _records(buf, rec: int):
     import numpy as np
     return np.frombuffer(buf, dtype=np.uint8).reshape(-1, rec)

@@ -51,6 +51,9 @@ SIGNATURES = {
     "kzgpot_preprocess_ex": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_uint32, ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, intp, i64p]),
     "kzgpot_preprocess_buffer_ex": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32, ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, intp, i64p]),
     "kzgpot_blake2b": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
+    "kzgpot_bn254_g1_decompress": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, i64p]),
+    "kzgpot_bn254_g1_decompress_ex": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, i64p, ctypes.c_void_p]),
+    "kzgpot_bn254_g1_decompress_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "kzgpot_status_name": (ctypes.c_char_p, [ctypes.c_int]),
     "kzgpot_device_count": (ctypes.c_int, []),
     "kzgpot_version": (ctypes.c_char_p, []),

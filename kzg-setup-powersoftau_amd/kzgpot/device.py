@@ -22,7 +22,7 @@ def synth_lib() -> ctypes.CDLL:
         if not os.path.exists(SYNTH_PATH):
             raise OSError(f"{SYNTH_PATH} not built")
         lib = ctypes.CDLL(SYNTH_PATH, mode=ctypes.RTLD_GLOBAL)
-        for name in ("kzgpot_synth_g1_dev", "kzgpot_synth_g2_dev"):
+        for name in ("kzgpot_synth_g1_dev", "kzgpot_synth_g2_dev", "kzgpot_synth_bn254_dev"):
             fn = getattr(lib, name)
             fn.restype = ctypes.c_int
             fn.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p,
@@ -37,10 +37,10 @@ def _stream() -> int:
 
 def synth(kind: str, seed: int, start: int, n: int, device, with_expected: bool = True):
     """Points start..start+n-1 of synthetic stream `seed`: (compressed, expected ark bytes)."""
-    rin, rout = (48, 96) if kind == "g1" else (96, 192)
+    rin, rout = {"g1": (48, 96), "g2": (96, 192), "bn254": (32, 64)}[kind]
     comp = torch.empty(max(1, n * rin), dtype=torch.uint8, device=device)
     ark = torch.empty(max(1, n * rout), dtype=torch.uint8, device=device) if with_expected else None
-    fn = synth_lib().kzgpot_synth_g1_dev if kind == "g1" else synth_lib().kzgpot_synth_g2_dev
+    fn = getattr(synth_lib(), f"kzgpot_synth_{kind}_dev")
     rc = fn(seed, start, n, comp.data_ptr(), ark.data_ptr() if ark is not None else None, _stream())
     if rc:
         raise RuntimeError(f"synth {kind} failed: {rc}")
@@ -54,6 +54,7 @@ _DEV_FNS = {
     "g2_transcode": ("kzgpot_g2_transcode_uncompressed_dev", 192, 192),
     "g1_load": ("kzgpot_g1_deserialize_unchecked_dev", 96, 104),   # no flags argument
     "g2_load": ("kzgpot_g2_deserialize_unchecked_dev", 192, 200),
+    "bn254_g1_decompress": ("kzgpot_bn254_g1_decompress_dev", 32, 64),  # no flags argument
 }
 
 
@@ -69,7 +70,7 @@ def codec_dev(op: str, d_in: torch.Tensor, d_out: torch.Tensor, key: torch.Tenso
         raise ValueError("codec_dev needs device tensors")
     st = d_status.data_ptr() if d_status is not None else None
     fn = getattr(_lib.load(), fname)
-    if op.endswith("_load"):
+    if op.endswith("_load") or op.startswith("bn254"):
         rc = fn(d_in.data_ptr(), n, d_out.data_ptr(), key.data_ptr(), st, _stream())
     else:
         rc = fn(d_in.data_ptr(), n, d_out.data_ptr(), flags, key.data_ptr(), st, _stream())

@@ -546,6 +546,88 @@ def load_fastkzg_setup(data: bytes, n: int):
     return OK, tuple(outs)
 
 
+# ----------------------------------------------------------------------------------------------
+# BN254 G1 (config 5, SURVEY §8f 4 — no reference counterpart): ark-bn254 0.2 compressed G1
+# → ark-ec 0.2 GroupAffine::deserialize → serialize_uncompressed. Same ark rules as the BLS12-381
+# read path above (SWFlags, Fp < p), plus ark's compressed branch: Infinity → zero(); else
+# get_point_from_x(x, PositiveY) with the `(y < -y) ^ greatest` rule; cofactor 1.
+# ----------------------------------------------------------------------------------------------
+BN_P = 0x30644E72E131A029B85045B68181585D97816A916871CA8D3C208C16D87CFD47
+BN_R = 0x30644E72E131A029B85045B68181585D2833E84879B9709143E1F593F0000001
+BN_B = 3
+BN_G1_GEN = (1, 2)
+
+
+def bn_sqrt(a):
+    a %= BN_P
+    y = pow(a, (BN_P + 1) // 4, BN_P)
+    return y if y * y % BN_P == a else None
+
+
+def bn_on_curve(pt):
+    x, y = pt
+    return (y * y - x * x * x - BN_B) % BN_P == 0
+
+
+def bn_add(a, b):
+    if a is None:
+        return b
+    if b is None:
+        return a
+    (x1, y1), (x2, y2) = a, b
+    if x1 == x2:
+        if (y1 + y2) % BN_P == 0:
+            return None
+        lam = 3 * x1 * x1 * pow(2 * y1, -1, BN_P) % BN_P
+    else:
+        lam = (y2 - y1) * pow(x2 - x1, -1, BN_P) % BN_P
+    x3 = (lam * lam - x1 - x2) % BN_P
+    return (x3, (lam * (x1 - x3) - y1) % BN_P)
+
+
+def bn_mul(pt, k):
+    acc = None
+    for bit in bin(k)[2:] if k > 0 else "":
+        acc = bn_add(acc, acc)
+        if bit == "1":
+            acc = bn_add(acc, pt)
+    return acc
+
+
+def bn254_g1_compress(pt) -> bytes:
+    """ark-ec 0.2 `serialize` (compressed): x LE + SWFlags (PositiveY iff y > -y; zero → Infinity)."""
+    if pt is None:
+        return bytes(31) + b"\x40"
+    x, y = pt
+    b = bytearray(x.to_bytes(32, "little"))
+    if y > (BN_P - y) % BN_P:
+        b[31] |= 0x80
+    return bytes(b)
+
+
+def bn254_g1_decompress_point(enc32: bytes):
+    """ark-bn254 G1Affine::deserialize (compressed) → serialize_uncompressed. (status, 64 B | None)."""
+    b = bytearray(enc32)
+    top = b[31]
+    pos, inf = bool(top >> 7 & 1), bool(top >> 6 & 1)
+    if pos and inf:
+        return E_UNEXPECTED_FLAGS, None
+    b[31] &= 0x3F
+    x = int.from_bytes(b, "little")
+    if x >= BN_P:
+        return E_NOT_IN_FIELD, None
+    if inf:
+        out = bytearray(bytes(32) + (1).to_bytes(32, "little"))
+        out[63] |= 0x40
+        return OK, bytes(out)
+    y = bn_sqrt(x * x * x + BN_B)
+    if y is None:
+        return E_NOT_ON_CURVE, None
+    negy = (BN_P - y) % BN_P
+    y = y if (y < negy) ^ pos else negy
+    return OK, x.to_bytes(32, "little") + y.to_bytes(32, "little")
+
+
 def batch(fn, data: bytes, rec: int, out_rec: int, **kw):
     """Apply a per-point function over a packed stream → (out bytes, statuses, first_bad)."""
     n = len(data) // rec

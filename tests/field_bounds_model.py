@@ -24,8 +24,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CONSTS = os.path.join(HERE, "..", "kzg-setup-powersoftau_amd", "csrc", "bls12_381_consts.hpp")
 
 
-def _load_consts():
-    text = open(CONSTS).read()
+def _load_consts(path=CONSTS):
+    text = open(path).read()
     out = {}
     for name, body in re.findall(r"static constexpr uint32_t (\w+)\[\d+\] = \{([^}]*)\}", text):
         out[name] = [int(v.strip().rstrip("u"), 16) for v in body.split(",")]
@@ -33,6 +33,22 @@ def _load_consts():
 
 
 C = _load_consts()
+
+FIELDS = {
+    "bls12_381": (P, 14, "bls12_381_consts.hpp"),
+    "bn254": (0x30644E72E131A029B85045B68181585D97816A916871CA8D3C208C16D87CFD47, 10, "bn254_consts.hpp"),
+}
+
+
+def use_field(name):
+    """Re-point the model at another field (the device code is generic over the traits struct)."""
+    global P, NL, R, P_L, P_OVER_R, P_TOP, C
+    P, NL, hdr = FIELDS[name]
+    R = 1 << (LB * NL)
+    P_L = [(P >> (LB * i)) & LM for i in range(NL)]
+    P_OVER_R = P / R * UP
+    P_TOP = P / (1 << (LB * (NL - 1))) * UP
+    C = _load_consts(os.path.join(os.path.dirname(CONSTS), hdr))
 
 
 class BoundError(AssertionError):

@@ -9,6 +9,8 @@ Vectors (all seeded, deterministic):
   g2_transcode.json    pairing-uncompressed G2 → ark (read_g2, src/lib.rs:56-80)
   g1_load.json         ark uncompressed G1 → in-memory GroupAffine (deserialize_unchecked, the
   g2_load.json         load_kzg_setup / load_fastkzg_setup loaders, src/lib.rs:174-228)
+  bn254_g1_decompress.json  config 5: ark-bn254 compressed G1 → ark uncompressed (no reference
+                       counterpart; pinned by the BN254 spec constants and the ark format rules)
   transcript_n1024.bin a powersoftau response file for N = 2^10 (config 1), + expected digests of
                        the kgz / fastkgz outputs in transcript_n1024.json
 
@@ -285,6 +287,45 @@ def g2_load_vectors(rng):
     return V
 
 
+def bn254_vectors(rng):
+    V = []
+
+    def add(b, note):
+        st, out = O.bn254_g1_decompress_point(b)
+        V.append(vec("bn", b, st, out, note))
+
+    BP = O.BN_P
+    add(O.bn254_g1_compress(O.BN_G1_GEN), "generator (1, 2)")
+    for i in range(40):
+        add(O.bn254_g1_compress(O.bn_mul(O.BN_G1_GEN, rng.randrange(1, O.BN_R))), f"random point {i}")
+    q = O.bn_mul(O.BN_G1_GEN, 4242)
+    b = bytearray(O.bn254_g1_compress(q))
+    b[31] ^= 0x80
+    add(bytes(b), "PositiveY flipped (= -P)")
+    add(O.bn254_g1_compress(None), "infinity (ark zero)")
+    add((5).to_bytes(32, "little")[:31] + b"\x40", "infinity flag with x = 5: zero()")
+    b = bytearray((BP - 1).to_bytes(32, "little"))
+    b[31] |= 0x40
+    add(bytes(b), "infinity flag with x = p - 1: zero()")
+    b = bytearray(BP.to_bytes(32, "little"))
+    b[31] |= 0x40
+    add(bytes(b), "infinity flag with x = p: InvalidData")
+    b = bytearray(O.bn254_g1_compress(q))
+    b[31] |= 0xC0
+    add(bytes(b), "both SW flags: UnexpectedFlags")
+    for note, x in (("x = p", BP), ("x = p + 1", BP + 1), ("x = 2^254 - 1", (1 << 254) - 1)):
+        add(x.to_bytes(32, "little"), note + ": not in field")
+    nres = 0
+    while nres < 6:
+        x = rng.randrange(BP)
+        if O.bn_sqrt(x ** 3 + 3) is None:
+            b = bytearray(x.to_bytes(32, "little"))
+            b[31] |= 0x80 if nres % 2 else 0
+            add(bytes(b), "x^3+3 non-residue: NotOnCurve")
+            nres += 1
+    return V
+
+
 def main():
     rng = random.Random(20261015)
     for name, fn in (("g1_decompress", g1_vectors), ("g2_decompress", g2_vectors),
@@ -295,7 +336,8 @@ def main():
                        "vectors": V}, f, indent=0)
         print(name, len(V), "vectors;", sum(v["status"] == 0 for v in V), "accepted")
     rng = random.Random(20261016)  # separate stream: the loader vectors came later
-    for name, fn in (("g1_load", g1_load_vectors), ("g2_load", g2_load_vectors)):
+    for name, fn in (("g1_load", g1_load_vectors), ("g2_load", g2_load_vectors),
+                     ("bn254_g1_decompress", bn254_vectors)):
         V = fn(rng)
         with open(os.path.join(HERE, name + ".json"), "w") as f:
             json.dump({"generator": "tests/golden/make_golden.py", "oracle": "oracle/kzgpot_oracle.py",

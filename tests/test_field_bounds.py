@@ -124,3 +124,23 @@ def test_loader_conversion():
     """load_kernels.hip words_to_ark_mont: canonical x (< p) times FP_ARK_R, one reduction."""
     k = M.const(M.C["FP_ARK_R"])
     M.reduce_once_ok(M.mul(M.normalized(1), k))
+
+
+@pytest.fixture
+def bn254_model():
+    M.use_field("bn254")
+    yield M
+    M.use_field("bls12_381")
+
+
+def test_bn254_decompress_chain(bn254_model):
+    """bn254_kernels.hip: x < 2^254 (< 1.33 p), a = x^3 + 3, the (p-3)/4 chain, y^2 == a
+    against KB_EQ (= 8p, borrowed with 2^28 limbs), from_mont; ark Montgomery output."""
+    x = M.normalized(Fraction(133, 100))
+    xm = M.mul(x, M.normalized(1), "to_mont")
+    a = M.norm(M.add_nr(M.mul(M.sqr(xm), xm), M.normalized(1)))
+    t = _pow_pm3d4(a)
+    y = M.mul(t, a, "y")
+    M.canon_ok(M.subk(M.sqr(y), a, "KB_EQ"), "fp_eq")
+    M.from_mont_ok(y)
+    M.reduce_once_ok(M.mul(M.normalized(1), M.const(M.C["BN_ARK_R"])))

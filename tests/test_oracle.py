@@ -177,3 +177,17 @@ def test_load_setup_digests(oracle_lib):
         assert hashlib.blake2b(b"".join(parts)).hexdigest() == meta[key]
     with pytest.raises(ValueError):
         O.load_kzg_setup(b"\x00" * 100, n)
+
+
+def test_bn254_spec_and_golden():
+    """Config 5 (BN254, no reference counterpart): the curve constants and the ark rules."""
+    assert O.BN_P % 4 == 3 and O.BN_P.bit_length() == 254 and O.BN_R.bit_length() == 254
+    assert O.bn_on_curve(O.BN_G1_GEN) and O.bn_mul(O.BN_G1_GEN, O.BN_R) is None
+    for v in golden("bn254_g1_decompress"):
+        st, out = O.bn254_g1_decompress_point(bytes.fromhex(v["in"]))
+        assert st == v["status"] and (out.hex() if out else None) == v["out"], v["note"]
+        if st == 0 and not (bytes.fromhex(v["in"])[31] & 0x40):
+            x = int.from_bytes(out[:32], "little")
+            y = int.from_bytes(out[32:], "little")
+            assert O.bn_on_curve((x, y))
+            assert O.bn254_g1_compress((x, y)) == bytes.fromhex(v["in"])  # round trip

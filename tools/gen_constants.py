@@ -24,11 +24,16 @@ import kzgpot_oracle as O  # noqa: E402
 
 P, R, U = O.P, O.R_ORDER, O.U_PARAM
 LB = 28                 # limb bits
-NL = 14                 # limbs
+NL = 14                 # limbs (BLS12-381)
 RM = 1 << (LB * NL)     # Montgomery R = 2^392
 W = 4                   # sqrt sliding window
 # (c, L) borrowed multiples used by the formulas in csrc/curve.hpp / fp381.hpp
 KB = [(2, 28), (4, 28), (8, 28), (8, 29), (16, 28), (32, 28), (32, 29), (64, 28), (64, 29), (64, 31), (128, 28), (128, 31)]
+
+# BN254 base field (config 5; ark-bn254 0.2 Fq): 10 x 28-bit limbs, R = 2^280
+BN_P = 0x30644E72E131A029B85045B68181585D97816A916871CA8D3C208C16D87CFD47
+BN_R = 0x30644E72E131A029B85045B68181585D2833E84879B9709143E1F593F0000001
+BN_NL = 10
 
 
 def limbs28(x, n=NL):
@@ -48,20 +53,23 @@ def mont(x):
     return x * RM % P
 
 
-def borrowed(c, L):
-    k = limbs28(c * P)
-    assert sum(v << (LB * i) for i, v in enumerate(k)) == c * P
+def borrowed(c, L, p=None, nl=NL, vmax=None):
+    """c p in the borrowed limb form; its top limb must dominate the top limb of any normalized
+    subtrahend of value < vmax p (default c - 0.001)."""
+    p = P if p is None else p
+    vmax = c - 0.001 if vmax is None else vmax
+    k = limbs28(c * p, nl)
+    assert sum(v << (LB * i) for i, v in enumerate(k)) == c * p
     hi, lo = 1 << L, 1 << (L - LB)
     out = list(k)
     out[0] += hi
-    for i in range(1, NL - 1):
+    for i in range(1, nl - 1):
         out[i] += hi - lo
-    out[NL - 1] -= lo
-    assert sum(v << (LB * i) for i, v in enumerate(out)) == c * P
-    assert all(v < (1 << 32) for v in out)
-    assert min(out[: NL - 1]) >= hi - lo
-    # the top limb must dominate the top limb of any subtrahend of value < (c - 0.001) p
-    assert out[NL - 1] >= ((c * 1000 - 1) * P // 1000) >> (LB * (NL - 1)), (c, L)
+    out[nl - 1] -= lo
+    assert sum(v << (LB * i) for i, v in enumerate(out)) == c * p
+    assert all(0 <= v < (1 << 32) for v in out)
+    assert min(out[: nl - 1]) >= hi - lo
+    assert out[nl - 1] >= int(vmax * 1000) * p // 1000 >> (LB * (nl - 1)), (c, L)
     return out
 
 
@@ -102,9 +110,47 @@ def sliding_window(e, w):
     return steps
 
 
+def field_struct(name, p, nl, nw, kb, comment):
+    """Field parameters as a traits struct consumed by the generic field core (csrc/fp381.hpp)."""
+    rm = 1 << (LB * nl)
+    assert p % 4 == 3 and p < rm // 2048
+    pinv = (-pow(p, -1, 1 << LB)) % (1 << LB)
+    steps = sliding_window((p - 3) // 4, W)
+    nmul = sum(1 for st in steps if st[1] >= 0) - 1
+    nsq = sum(st[0] for st in steps)
+    L = [f"// {comment}: {nl} x {LB}-bit limbs, Montgomery R = 2^{LB * nl}.",
+         f"struct {name} {{",
+         f"  static constexpr int NL = {nl};  // limbs",
+         f"  static constexpr int NW = {nw};  // 32-bit words of a serialized coordinate",
+         "  " + arr("P", limbs28(p, nl)),
+         f"  static constexpr uint32_t PINV = 0x{pinv:07x}u;  // -p^-1 mod 2^28",
+         "  " + arr("R2", limbs28(rm * rm % p, nl), "R^2 mod p"),
+         "  " + arr("ONE", limbs28(rm % p, nl), "R mod p (Montgomery 1)")]
+    for c in (1, 2, 4, 8, 16, 32, 64, 128):
+        L.append("  " + arr(f"P_X{c}", limbs28(c * p, nl), f"{c} p, normalized (canonical reduction)"))
+    for c, Lb, vmax, alias in kb:
+        nm = alias or f"KB_{c}_{Lb}"
+        L.append("  " + arr(nm, borrowed(c, Lb, p, nl, vmax),
+                            f"{c} p, limbs >= 2^{Lb} - 2^{Lb - LB}, dominates values < {vmax if vmax else c - 0.001} p"))
+    L += ["  " + arr("P_WORDS", words32(p, nw), f"p as {nw} x 32-bit words (byte-level range checks)"),
+          f"  // a^((p-3)/4): sliding window w={W}, table a, a^3, .., a^{2 ** W - 1}; {nsq} squarings + {nmul} "
+          f"multiplications after the table ({2 ** (W - 1)} entries).",
+          f"  static constexpr int SQRT_TABLE = {2 ** (W - 1)};",
+          f"  static constexpr int SQRT_STEPS = {len(steps)};",
+          "  static constexpr int8_t SQRT_STEP_SQ[SQRT_STEPS] = {" + ", ".join(str(st[0]) for st in steps) + "};",
+          "  static constexpr int8_t SQRT_STEP_IDX[SQRT_STEPS] = {" + ", ".join(str(st[1]) for st in steps) + "};",
+          "};"]
+    return L, nsq, nmul
+
+
+def write(fname, lines):
+    out = os.path.join(HERE, "..", "kzg-setup-powersoftau_amd", "csrc", fname)
+    with open(out, "w") as f:
+        f.write("\n".join(lines))
+    print("wrote", out)
+
+
 def main():
-    assert P % 4 == 3 and P < RM // 2048
-    pinv = (-pow(P, -1, 1 << LB)) % (1 << LB)
     lam = (-U * U) % R
     q = O.g1_mul(O.G1_GEN, lam)
     beta = None
@@ -124,35 +170,24 @@ def main():
     psi = (O.fp2_mul(O.fp2_conj(O.G2_GEN[0]), cx), O.fp2_mul(O.fp2_conj(O.G2_GEN[1]), cy))
     assert psi == O.g2_mul(O.G2_GEN, U)
     assert cx[0] == 0  # purely imaginary: conj(x) * (0 + c u) = (x1 c, x0 c)
-    e = (P - 3) // 4
-    steps = sliding_window(e, W)
-    nmul = sum(1 for s in steps if s[1] >= 0) - 1
-    nsq = sum(s[0] for s in steps)
     inv2 = pow(2, P - 2, P)
     absu = -U
+    bls_kb = [(c, Lb, None, None) for c, Lb in KB] + [(64, 31, None, "KB_EQ")]
+    fs, nsq, nmul = field_struct("BlsFp", P, NL, 12, bls_kb, "BLS12-381 Fq")
     lines = [
         "// GENERATED by tools/gen_constants.py — do not edit by hand.",
-        f"// BLS12-381 constants: {NL} x {LB}-bit limbs, Montgomery R = 2^{LB * NL}.",
         "#pragma once",
         "#include <stdint.h>",
         "namespace kzgpot {",
-        arr("FP_P", limbs28(P)),
-        f"static constexpr uint32_t FP_PINV = 0x{pinv:07x}u;  // -p^-1 mod 2^28",
-        arr("FP_R2", limbs28(RM * RM % P), "R^2 mod p"),
-        arr("FP_ONE", limbs28(mont(1)), "R mod p (Montgomery 1)"),
+    ] + fs + [
+        "// BLS12-381 curve constants (Montgomery form of BlsFp unless noted)",
         arr("FP_FOUR", limbs28(mont(4))),
+        arr("FP_ARK_R", limbs28((1 << 384) * RM % P), "2^384 R mod p: fp_mul(x, .) = x 2^384 (ark-ff Montgomery form)"),
         arr("FP_INV2", limbs28(mont(inv2))),
         arr("FP_BETA", limbs28(mont(beta))),
         arr("FP_PSI_CX1", limbs28(mont(cx[1]))),
         arr("FP_PSI_CY0", limbs28(mont(cy[0]))),
         arr("FP_PSI_CY1", limbs28(mont(cy[1]))),
-    ]
-    for c in (1, 2, 4, 8, 16, 32, 64, 128):
-        lines.append(arr(f"FP_P_X{c}", limbs28(c * P), f"{c} p, normalized (canonical reduction)"))
-    for c, L in KB:
-        lines.append(arr(f"KB_{c}_{L}", borrowed(c, L), f"{c} p with limbs >= 2^{L} - 2^{L - LB}"))
-    lines += [
-        arr("P_WORDS", words32(P), "p as 12 x 32-bit words (byte-level range checks)"),
         arr("G1_GEN_X", limbs28(mont(O.G1_GEN[0])), "Montgomery form (synthetic-data generator)"),
         arr("G1_GEN_Y", limbs28(mont(O.G1_GEN[1]))),
         arr("G2_GEN_X0", limbs28(mont(O.G2_GEN[0][0]))),
@@ -163,19 +198,31 @@ def main():
         "static constexpr int BLS_ABS_U_BITS = %d;" % absu.bit_length(),
         arr("FR_R", words32(R, 8), "group order r (ref-mode double-and-add)"),
         "static constexpr int FR_R_BITS = %d;" % R.bit_length(),
-        f"// a^((p-3)/4): sliding window w={W}, table = a^1, a^3, ..., a^{2 ** W - 1}; "
-        f"{nsq} squarings + {nmul} multiplications after the table ({2 ** (W - 1)} entries).",
-        f"static constexpr int SQRT_TABLE = {2 ** (W - 1)};",
-        f"static constexpr int SQRT_STEPS = {len(steps)};",
-        "static constexpr int8_t SQRT_STEP_SQ[SQRT_STEPS] = {" + ", ".join(str(s[0]) for s in steps) + "};",
-        "static constexpr int8_t SQRT_STEP_IDX[SQRT_STEPS] = {" + ", ".join(str(s[1]) for s in steps) + "};",
         "}  // namespace kzgpot",
         "",
     ]
-    out = os.path.join(HERE, "..", "kzg-setup-powersoftau_amd", "csrc", "bls12_381_consts.hpp")
-    with open(out, "w") as f:
-        f.write("\n".join(lines))
-    print("wrote", out, f"sqrt chain: {nsq} sq + {nmul} mul + table {2 ** (W - 1) - 1} mul + 1 sq")
+    write("bls12_381_consts.hpp", lines)
+    print(f"  BLS12-381 sqrt chain: {nsq} sq + {nmul} mul + table {2 ** (W - 1) - 1} mul + 1 sq")
+
+    # BN254 (config 5): only the decompress chain runs here; fp_eq compares against normalized
+    # values < 4p, which KB_8_28 dominates even with the small top limb of a 254-bit p
+    bn_rm = 1 << (LB * BN_NL)
+    fs, nsq, nmul = field_struct("Bn254Fp", BN_P, BN_NL, 8, [(8, 28, 4, "KB_EQ")], "BN254 Fq (ark-bn254 0.2)")
+    lines = [
+        "// GENERATED by tools/gen_constants.py — do not edit by hand.",
+        "#pragma once",
+        "#include <stdint.h>",
+        "namespace kzgpot {",
+    ] + fs + [
+        "// BN254 G1: y^2 = x^3 + 3, cofactor 1",
+        arr("BN_THREE", limbs28(3 * bn_rm % BN_P, BN_NL), "3 R mod p"),
+        arr("BN_ARK_R", limbs28((1 << 256) * bn_rm % BN_P, BN_NL), "2^256 R mod p (ark-ff Fp256 Montgomery form)"),
+        arr("BN_FR_R", words32(BN_R, 8), "group order r"),
+        "}  // namespace kzgpot",
+        "",
+    ]
+    write("bn254_consts.hpp", lines)
+    print(f"  BN254 sqrt chain: {nsq} sq + {nmul} mul")
 
 
 if __name__ == "__main__":
