@@ -95,3 +95,64 @@ def test_smoke_entry(gpu):
     import __graft_entry__
 
     __graft_entry__.smoke()
+
+
+def _corrupt(buf: bytearray, rec: int, n: int, seed: int, every: int = 997):
+    """Deterministically damage ~1/every records in the ways the reference rejects (or, for a
+    flipped 'greatest' bit, decodes differently)."""
+    import random
+
+    rng = random.Random(seed)
+    for i in range(rng.randrange(every), n, every):
+        o = i * rec
+        kind = rng.randrange(5)
+        if kind == 0:
+            buf[o] ^= 0x20                       # greatest flipped: valid, the other root
+        elif kind == 1:
+            buf[o] &= 0x7F                       # not compressed
+        elif kind == 2:
+            buf[o + rec - 1] ^= 1 << rng.randrange(8)  # x perturbed: non-residue or non-subgroup
+        elif kind == 3:
+            buf[o:o + 48] = bytes([0x9F]) + b"\xff" * 47   # x >= p
+        else:
+            buf[o] |= 0x40                       # infinity bit with stray bits
+
+
+def test_config2_g1_2e20_vs_cpu(dev, oracle_lib):
+    """BASELINE config 2: 2^20 G1, decompress + subgroup check on 1 MI355X, bit-exact vs the CPU
+    restatement on every point (bytes, per-point status, first bad index), with ~0.1 % damage."""
+    torch, D = dev
+    n = 1 << 20
+    comp, _ = D.synth("g1", 2020, 0, n, "cuda", with_expected=False)
+    data = bytearray(comp.cpu().numpy().tobytes())
+    _corrupt(data, 48, n, 1)
+    import kzgpot
+
+    g = kzgpot.g1_decompress(bytes(data), want_status=True)
+    out, st, fb, r = oracle_run(oracle_lib, "g1_decompress", bytes(data), n, threads=16)
+    assert g.status == st and g.first_bad == fb and g.ret == r
+    assert g.out == out
+    assert 0 < sum(s != 0 for s in st) < n // 500
+
+
+def test_config3_g1_g2_2e20(dev, oracle_lib):
+    """BASELINE config 3: 2^20 G1 + 2^20 G2 on 1 MI355X: every point against the generator's
+    expected bytes (decode(encode(P)) = P), and a damaged 2^12-point G2 slice against the CPU
+    restatement (bytes + statuses)."""
+    torch, D = dev
+    n = 1 << 20
+    key = torch.empty(1, dtype=torch.int64, device="cuda")
+    for kind, rin, rout in (("g1", 48, 96), ("g2", 96, 192)):
+        comp, exp = D.synth(kind, 3030, 0, n, "cuda")
+        out = torch.empty(n * rout, dtype=torch.uint8, device="cuda")
+        D.codec_dev(f"{kind}_decompress", comp, out, key)
+        assert D.read_key(key) == (1 << 64) - 1
+        assert torch.equal(out, exp)
+    import kzgpot
+
+    m = 1 << 12
+    data = bytearray(comp[: m * 96].cpu().numpy().tobytes())
+    _corrupt(data, 96, m, 2, every=97)
+    g = kzgpot.g2_decompress(bytes(data), want_status=True)
+    out, st, fb, r = oracle_run(oracle_lib, "g2_decompress", bytes(data), m, threads=16)
+    assert g.status == st and g.first_bad == fb and g.ret == r and g.out == out
