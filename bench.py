@@ -51,6 +51,7 @@ def parse():
     ap.add_argument("--cpu-sample-log2", type=int, default=15)
     ap.add_argument("--no-next-rows", action="store_true", help="skip the loader / BN254 (SURVEY 8f) measurements")
     ap.add_argument("--bn254-log2", type=int, default=28, help="config 5 size (0 = skip)")
+    ap.add_argument("--e2e-log2", type=int, default=21, help="end-to-end preprocess N (0 = skip)")
     return ap.parse_args()
 
 
@@ -92,6 +93,39 @@ def pmc_traffic(n_g1_local):
         return d["g1_bytes_per_point"] * n_g1_local
     except Exception:
         return None
+
+
+def e2e_preprocess(n_log2, seed, dev, kzgpot, D):
+    """Build a synthetic response transcript (powersoftau layout, GPU-generated valid points) and
+    time kzgpot_preprocess_buffer_ex on it in both modes; check the τG1 / ατG1 sections."""
+    import torch
+
+    n = 1 << n_log2
+    parts, expect = [torch.zeros(64, dtype=torch.uint8, device=dev)], {}
+    for name, kind, cnt in (("tau_g1", "g1", 2 * n - 1), ("tau_g2", "g2", n), ("alpha_g1", "g1", n),
+                            ("beta_g1", "g1", n), ("beta_g2", "g2", 1)):
+        c, e = D.synth(kind, seed + len(parts), 0, cnt, dev, with_expected=name in ("tau_g1", "alpha_g1"))
+        parts.append(c)
+        if e is not None:
+            expect[name] = e.cpu().numpy().tobytes()
+    parts.append(torch.zeros(3 * 192 + 6 * 96, dtype=torch.uint8, device=dev))
+    tr = torch.cat(parts).cpu().numpy().tobytes()
+    del parts
+    assert len(tr) == kzgpot.contribution_size(n_log2)
+    rows = {}
+    for mode, name in ((kzgpot.MODE_KZG, "preprocess_kgz_e2e"), (kzgpot.MODE_FASTKZG, "preprocess_fastkgz_e2e")):
+        t0 = time.perf_counter()
+        res = kzgpot.preprocess_buffer(tr, n_log2, mode, n_gpus=1, with_digests=True)
+        dt = time.perf_counter() - t0
+        g1n = (2 * n - 1) * 96
+        ok = res.out[:g1n] == expect["tau_g1"] and res.out[g1n:g1n + n * 96] == expect["alpha_g1"]
+        pts = (2 * n - 1) + 3 * n + 1
+        rows[name] = {"workload": f"N = 2^{n_log2} response transcript ({len(tr)} B) -> {len(res.out)} B file, "
+                                  "host buffers, 1 GPU, BLAKE2b of input and output",
+                      "seconds": dt, "points": pts, "points_per_s": pts / dt, "sections_verified": bool(ok),
+                      "transcript_blake2b": res.transcript_digest[:16] + "...",
+                      "output_blake2b": res.output_digest[:16] + "..."}
+    return rows
 
 
 def main():
@@ -234,6 +268,10 @@ def main():
                 "hbm_frac": 96 * nb / (bn_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                 "verified_bit_exact": bool(ok), "generate_s": t_bn}
             del compb, expb, outb
+        # end-to-end preprocess (host transcript in → host kgz / fastkzg file
+        # out, PCIe both ways, BLAKE2b of both on host threads) at the reference's N = 2^21
+        if world == 1 and args.e2e_log2 > 0:
+            next_rows.update(e2e_preprocess(args.e2e_log2, args.seed + 3, dev, kzgpot, D))
 
     g1_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / len(ev)
     g2_ms = sum(e[1].elapsed_time(e[2]) for e in ev) / len(ev)
