@@ -78,57 +78,63 @@ KZG_DEV void jac_dbl(jac<fp>& p) {
   fp_subk_nr(p.y, t, c8, BlsFp::KB_8_29); // Y3 = E (D - X3) - 8C  < 2^30
 }
 
-// Generic (Fp2, cold): all values reduced (< 2p) through the Fp2 helpers above.
+// Generic (Fp2, cold): all values reduced (< 2p) through the Fp2 helpers above. Ordered so
+// that each input dies as early as possible (Y after B and Z3, X after A and D): at most five
+// Fp2 temporaries live beside the Karatsuba scratch, which keeps the G2 kernels off AGPR spills.
 template <typename F>
 KZG_DEV void jac_dbl(jac<F>& p) {
-  F a, b, c8, d, e, t;
-  f_sqr(a, p.x);
-  f_sqr(b, p.y);
-  f_shl<3>(t, b);
-  f_norm(t, t);
-  f_mul(c8, t, b);             // 8C
-  f_shl<2>(t, p.x);
-  f_norm(t, t);
-  f_mul(d, t, b);              // D = 4XB
-  f_mul3(e, a);
-  f_norm(e, e);                // E = 3A
+  F b, t, a, d, c8;
+  f_sqr(b, p.y);               // B = Y^2
   f_shl<1>(t, p.y);
   f_norm(t, t);
-  f_mul(p.z, t, p.z);          // Z3 = 2YZ
-  f_sqr(a, e);                 // F
-  f_shl<1>(t, d);
-  f_subk(p.x, a, t, BlsFp::KB_64_29);
-  f_norm(p.x, p.x);            // X3 = F - 2D
-  f_mul3(t, d);
-  f_subk(t, t, a, BlsFp::KB_16_28);
-  f_norm(t, t);                // 3D - F
-  f_mul(t, e, t);
+  f_mul(p.z, t, p.z);          // Z3 = 2YZ           (Y dead)
+  f_sqr(a, p.x);               // A = X^2
+  f_shl<2>(t, p.x);
+  f_norm(t, t);
+  f_mul(d, t, b);              // D = 4XB            (X dead)
+  f_shl<3>(t, b);
+  f_norm(t, t);
+  f_mul(c8, t, b);             // 8C = 8B^2          (B dead)
+  f_mul3(a, a);
+  f_norm(a, a);                // E = 3A             (A dead)
+  f_sqr(t, a);                 // F = E^2
+  f_shl<1>(p.y, d);
+  f_subk(p.x, t, p.y, BlsFp::KB_64_29);
+  f_norm(p.x, p.x);            // X3 = F - 2D        (F dead)
+  f_subk(t, d, p.x, BlsFp::KB_128_28);
+  f_norm(t, t);                // D - X3            (D dead)
+  f_mul(t, a, t);
   f_subk(p.y, t, c8, BlsFp::KB_32_28);
-  f_norm(p.y, p.y);            // Y3
+  f_norm(p.y, p.y);            // Y3 = E (D - X3) - 8C
 }
 
 // ---------------------------------------------------------------- mixed addition (cold)
-// ark add_assign_mixed: p += (x2, y2) for a finite affine (x2, y2) (normalized, v <= 2).
+// ark add_assign_mixed: p += (x2, y2) for a finite affine (x2, y2) (normalized, v <= 2) that
+// `load(x2, y2)` delivers. The base point is fetched inside and dies after U2 / S2 (the rare
+// `self.is_zero()` branch fetches it again), so it never occupies registers across the formula.
 // In: X, Y limbs < 2^30, values <= 40; Z normalized. Out: normalized, values <= 64.
-template <typename F>
-KZG_DEV void jac_madd(jac<F>& p, const F& x2, const F& y2) {
+template <typename F, typename Load>
+KZG_DEV void jac_madd(jac<F>& p, Load&& load) {
   F z1z1, h, r, t;
-  f_sqr(z1z1, p.z);
-  f_mul(h, x2, z1z1);          // U2
-  f_subk(h, h, p.x, BlsFp::KB_128_31);
-  f_norm(h, h);                // H = U2 - X1
-  f_mul(t, y2, p.z);
-  f_mul(t, t, z1z1);           // S2
-  f_subk(r, t, p.y, BlsFp::KB_64_31);
-  f_norm(r, r);                // r' = S2 - Y1   (ark's r = 2 r')
+  {
+    F x2, y2;
+    load(x2, y2);
+    f_sqr(z1z1, p.z);
+    f_mul(h, x2, z1z1);        // U2
+    f_subk(h, h, p.x, BlsFp::KB_128_31);
+    f_norm(h, h);              // H = U2 - X1
+    f_mul(t, y2, p.z);
+    f_mul(t, t, z1z1);         // S2
+    f_subk(r, t, p.y, BlsFp::KB_64_31);
+    f_norm(r, r);              // r' = S2 - Y1   (ark's r = 2 r')
+  }
   const bool z1zero = f_is_zero(p.z);
   const bool same = !z1zero && f_is_zero(h) && f_is_zero(r);
   if (__builtin_expect(z1zero || same, 0)) {
     if (same) {
       jac_dbl(p);
     } else {
-      p.x = x2;
-      p.y = y2;
+      load(p.x, p.y);
       f_one(p.z);
     }
     return;
@@ -224,11 +230,7 @@ KZG_DEV void mul_abs_u_affine(jac<F>& acc, Load&& load) {
 #pragma unroll 1
   for (int b = BLS_ABS_U_BITS - 2; b >= 0; b--) {
     jac_dbl(acc);
-    if ((BLS_ABS_U >> b) & 1) {
-      F x, y;
-      load(x, y);
-      jac_madd(acc, x, y);
-    }
+    if ((BLS_ABS_U >> b) & 1) jac_madd(acc, load);
   }
 }
 // [|u|] q for Jacobian q
@@ -267,11 +269,7 @@ KZG_DEV bool in_subgroup_ref(Load&& load) {
   for (int b = FR_R_BITS - 2; b >= 0; b--) {
     jac_dbl(acc);
     const uint32_t word = FR_R[b >> 5];
-    if ((word >> (b & 31)) & 1) {
-      F x, y;
-      load(x, y);
-      jac_madd(acc, x, y);
-    }
+    if ((word >> (b & 31)) & 1) jac_madd(acc, load);
   }
   return f_is_zero(acc.z);
 }

@@ -94,7 +94,7 @@ __global__ void k_synth_table(uint32_t* __restrict__ table) {
   const int top = 31 - __builtin_clz(j);
   for (int b = top - 1; b >= 0; b--) {
     jac_dbl(acc);
-    if ((j >> b) & 1) jac_madd(acc, gx, gy);
+    if ((j >> b) & 1) jac_madd(acc, [&](F& x, F& y) { x = gx, y = gy; });
   }
   for (int k = 0; k < 4 * w; k++) jac_dbl(acc);
   F x, y;
@@ -147,11 +147,11 @@ __global__ void __launch_bounds__(kSynthBlock) k_synth(const uint32_t* __restric
   for (int w = 1; w < kWindows; w++) {
     const int d = (int)(((w < 16 ? klo >> (4 * w) : khi >> (4 * (w - 16)))) & 15);
     if (d) {
-      F tx, ty;
       const uint32_t* e = table + (size_t)(w * 16 + d) * 2 * words;
-      load_f(tx, e);
-      load_f(ty, e + words);
-      jac_madd(acc, tx, ty);
+      jac_madd(acc, [&](F& x, F& y) {
+        load_f(x, e);
+        load_f(y, e + words);
+      });
     }
   }
   F x, y;

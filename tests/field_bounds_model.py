@@ -293,20 +293,20 @@ def jac_dbl_fp(X, Y, Z):
 
 
 def jac_dbl_generic(F, X, Y, Z):
-    a = F.sqr(X, "A")
+    """curve.hpp jac_dbl<F> (the Fp2 instantiation; every op reduces)."""
     b = F.sqr(Y, "B")
-    t = F.norm(F.shl(b, 3))
-    c8 = F.mul(t, b, "8C")
-    t = F.norm(F.shl(X, 2))
-    d = F.mul(t, b, "D")
-    e = F.norm(F.mul3(a))
     t = F.norm(F.shl(Y, 1))
     z3 = F.mul(t, Z, "Z3")
-    a = F.sqr(e, "F")
-    t = F.shl(d, 1)
-    x3 = F.norm(F.subk(a, t, "KB_64_29", "X3"))
-    t = F.mul3(d)
-    t = F.norm(F.subk(t, a, "KB_16_28", "3D-F"))
+    a = F.sqr(X, "A")
+    t = F.norm(F.shl(X, 2))
+    d = F.mul(t, b, "D")
+    t = F.norm(F.shl(b, 3))
+    c8 = F.mul(t, b, "8C")
+    e = F.norm(F.mul3(a))
+    f = F.sqr(e, "F")
+    t2 = F.shl(d, 1)
+    x3 = F.norm(F.subk(f, t2, "KB_64_29", "X3"))
+    t = F.norm(F.subk(d, x3, "KB_128_28", "D-X3"))
     t = F.mul(e, t, "E(D-X3)")
     y3 = F.norm(F.subk(t, c8, "KB_32_28", "Y3"))
     return x3, y3, z3
