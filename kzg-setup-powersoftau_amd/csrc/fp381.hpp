@@ -210,11 +210,29 @@ KZG_DEV bool fp_is_zero_canon(const Fe<Tr>& c) {
   for (int i = 0; i < Tr::NL; i++) o |= c.v[i];
   return o == 0;
 }
+// a == 0 (mod p) for any a with limbs < 2^32 - 16 and value < 256 p (fp_canon's precondition),
+// without reducing: after normalization a is a multiple k p (k < 256) iff it equals k p for
+// k = floor((top + 1) 2^(28 (NL-1)) / p) — the only candidate, computed in double precision
+// (exact to ~1e-14 against a >= 4.6e-8 margin for every k; tests/test_fast_paths_math.py) — so
+// the test is one normalization, NL small MACs and a compare (~130 instructions) instead of the
+// 8-step conditional-subtraction chain (~600).
 template <class Tr>
 KZG_DEV bool fp_is_zero(const Fe<Tr>& a) {
-  Fe<Tr> c;
-  fp_canon(c, a);
-  return fp_is_zero_canon(c);
+  constexpr int N = Tr::NL;
+  Fe<Tr> n;
+  fp_norm(n, a);
+  const uint32_t k = (uint32_t)((double)(n.v[N - 1] + 1u) * Tr::INV_RHO);
+  uint64_t c = 0;
+  uint32_t diff = 0;
+#pragma unroll
+  for (int i = 0; i < N - 1; i++) {
+    c += (uint64_t)k * Tr::P[i];
+    diff |= ((uint32_t)c & LMASK) ^ n.v[i];
+    c >>= 28;
+  }
+  c += (uint64_t)k * Tr::P[N - 1];
+  diff |= (uint32_t)c ^ n.v[N - 1];
+  return diff == 0;
 }
 // a == b (mod p) for b dominated by Tr::KB_EQ (BLS: limbs < 2^31 - 8, value < 63 p;
 // BN254: normalized, value < 4 p)

@@ -125,7 +125,9 @@ def field_struct(name, p, nl, nw, kb, comment):
          "  " + arr("P", limbs28(p, nl)),
          f"  static constexpr uint32_t PINV = 0x{pinv:07x}u;  // -p^-1 mod 2^28",
          "  " + arr("R2", limbs28(rm * rm % p, nl), "R^2 mod p"),
-         "  " + arr("ONE", limbs28(rm % p, nl), "R mod p (Montgomery 1)")]
+         "  " + arr("ONE", limbs28(rm % p, nl), "R mod p (Montgomery 1)"),
+         f"  static constexpr double INV_RHO = {float((1 << (LB * (nl - 1))) / p)!r};  "
+         f"// 2^{LB * (nl - 1)} / p (fp_is_zero quotient estimate)"]
     for c in (1, 2, 4, 8, 16, 32, 64, 128):
         L.append("  " + arr(f"P_X{c}", limbs28(c * p, nl), f"{c} p, normalized (canonical reduction)"))
     for c, Lb, vmax, alias in kb:
