@@ -275,12 +275,25 @@ __global__ void __launch_bounds__(kBlock) k_g1_check(const uint4* __restrict__ i
   }
 
   if (st == 0 && !finf) {
-    auto load = [&](fp& bx, fp& by) {
+    // The base point in Montgomery form is parked in LDS (limb-major, so the 64 lanes of a wave
+    // hit 64 consecutive dwords): each of the ~8 reloads in the ladders is 28 LDS reads instead
+    // of two Montgomery conversions, and the point costs no VGPRs between reloads.
+    __shared__ uint32_t base[2 * NL][kBlock];
+    {
       words cx, cy;
-      G1Rec<S>::load_xy(cx, cy, opaque(rec));
+      G1Rec<S>::load_xy(cx, cy, rec);
       cy[11] &= 0x3fffffffu;
+      fp bx, by;
       words_to_mont(bx, cx);
       words_to_mont(by, cy);
+#pragma unroll
+      for (int k = 0; k < NL; k++) base[k][threadIdx.x] = bx.v[k], base[NL + k][threadIdx.x] = by.v[k];
+    }
+    auto load = [&](fp& bx, fp& by) {
+      uint32_t lane = threadIdx.x;
+      asm volatile("" : "+v"(lane));  // opaque index: re-read at every use, never hoisted
+#pragma unroll
+      for (int k = 0; k < NL; k++) bx.v[k] = base[k][lane], by.v[k] = base[NL + k][lane];
     };
     bool on_curve;
     {
