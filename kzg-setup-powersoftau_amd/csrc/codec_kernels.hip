@@ -345,7 +345,7 @@ struct G2Rec {
 };
 
 template <Src S>
-__global__ void __launch_bounds__(kBlock) k_g2_check(const uint4* __restrict__ in, uint4* __restrict__ out,
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 2))) k_g2_check(const uint4* __restrict__ in, uint4* __restrict__ out,
                                                      uint64_t n, uint32_t flags,
                                                      unsigned long long* __restrict__ first_bad,
                                                      uint8_t* __restrict__ status) {
@@ -373,14 +373,36 @@ __global__ void __launch_bounds__(kBlock) k_g2_check(const uint4* __restrict__ i
   }
 
   if (st == 0 && !finf) {
-    auto load = [&](fp2& bx, fp2& by) {
+    // Montgomery base point parked in LDS, limb-major (see k_g1_check)
+    __shared__ uint32_t base[4 * NL][kBlock];
+    {
       words x0, x1, y0, y1;
-      G2Rec<S>::load_xy(x0, x1, y0, y1, opaque(rec));
+      G2Rec<S>::load_xy(x0, x1, y0, y1, rec);
       y1[11] &= 0x3fffffffu;
-      words_to_mont(bx.c0, x0);
-      words_to_mont(bx.c1, x1);
-      words_to_mont(by.c0, y0);
-      words_to_mont(by.c1, y1);
+      fp t;
+      words_to_mont(t, x0);
+#pragma unroll
+      for (int k = 0; k < NL; k++) base[k][threadIdx.x] = t.v[k];
+      words_to_mont(t, x1);
+#pragma unroll
+      for (int k = 0; k < NL; k++) base[NL + k][threadIdx.x] = t.v[k];
+      words_to_mont(t, y0);
+#pragma unroll
+      for (int k = 0; k < NL; k++) base[2 * NL + k][threadIdx.x] = t.v[k];
+      words_to_mont(t, y1);
+#pragma unroll
+      for (int k = 0; k < NL; k++) base[3 * NL + k][threadIdx.x] = t.v[k];
+    }
+    auto load = [&](fp2& bx, fp2& by) {
+      uint32_t lane = threadIdx.x;
+      asm volatile("" : "+v"(lane));  // opaque index: re-read at every use, never hoisted
+#pragma unroll
+      for (int k = 0; k < NL; k++) {
+        bx.c0.v[k] = base[k][lane];
+        bx.c1.v[k] = base[NL + k][lane];
+        by.c0.v[k] = base[2 * NL + k][lane];
+        by.c1.v[k] = base[3 * NL + k][lane];
+      }
     };
     bool on_curve;
     {
