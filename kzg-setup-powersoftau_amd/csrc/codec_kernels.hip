@@ -278,7 +278,10 @@ __global__ void __launch_bounds__(kBlock) k_g1_check(const uint4* __restrict__ i
     // The base point in Montgomery form is parked in LDS (limb-major, so the 64 lanes of a wave
     // hit 64 consecutive dwords): each of the ~8 reloads in the ladders is 28 LDS reads instead
     // of two Montgomery conversions, and the point costs no VGPRs between reloads.
+    // The fast test's second ladder base Q1 = [|u|]P = (X : Y : Z) is parked beside it (qpark).
+    // 70 KB per 256-lane block: 2 blocks per CU, the occupancy the VGPR count allows anyway.
     __shared__ uint32_t base[2 * NL][kBlock];
+    __shared__ uint32_t qpark[3 * NL][kBlock];
     {
       words cx, cy;
       G1Rec<S>::load_xy(cx, cy, rec);
@@ -295,8 +298,10 @@ __global__ void __launch_bounds__(kBlock) k_g1_check(const uint4* __restrict__ i
 #pragma unroll
       for (int k = 0; k < NL; k++) bx.v[k] = base[k][lane], by.v[k] = base[NL + k][lane];
     };
-    bool on_curve;
-    {
+    // Phase 1 emits only points with y^2 = x^3 + 4 (it rejects non-residues), so an in-place
+    // record is on the curve; a transcode input may not be (the reference never checks).
+    bool on_curve = true;
+    if (S == Src::PairingBE) {
       fp xm, ym, l, r;
       load(xm, ym);
       fp_sqr(l, ym);
@@ -307,10 +312,31 @@ __global__ void __launch_bounds__(kBlock) k_g1_check(const uint4* __restrict__ i
       on_curve = fp_eq(l, r);
     }
     bool ok;
-    if ((flags & KZGPOT_SUBGROUP_REF) || !on_curve)
+    if ((flags & KZGPOT_SUBGROUP_REF) || !on_curve) {
       ok = in_subgroup_ref<fp>(load);
-    else
-      ok = in_subgroup_fast_g1(load);
+    } else {
+      auto park = [&](const jac<fp>& q) {
+#pragma unroll
+        for (int k = 0; k < NL; k++) {
+          qpark[k][threadIdx.x] = q.x.v[k];
+          qpark[NL + k][threadIdx.x] = q.y.v[k];
+          qpark[2 * NL + k][threadIdx.x] = q.z.v[k];
+        }
+      };
+      auto load_q = [&](fp& qx, fp& qy) {
+        uint32_t lane = threadIdx.x;
+        asm volatile("" : "+v"(lane));
+#pragma unroll
+        for (int k = 0; k < NL; k++) qx.v[k] = qpark[k][lane], qy.v[k] = qpark[NL + k][lane];
+      };
+      auto load_qz = [&](fp& qz) {
+        uint32_t lane = threadIdx.x;
+        asm volatile("" : "+v"(lane));
+#pragma unroll
+        for (int k = 0; k < NL; k++) qz.v[k] = qpark[2 * NL + k][lane];
+      };
+      ok = in_subgroup_fast_g1(load, park, load_q, load_qz);
+    }
     if (!ok) st = 5;
   }
   if (st) {

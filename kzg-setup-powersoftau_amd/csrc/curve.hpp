@@ -109,9 +109,10 @@ KZG_DEV void jac_dbl(jac<F>& p) {
 }
 
 // ---------------------------------------------------------------- mixed addition (cold)
-// ark add_assign_mixed: p += (x2, y2) for a finite affine (x2, y2) (normalized, v <= 2) that
-// `load(x2, y2)` delivers. The base point is fetched inside and dies after U2 / S2 (the rare
-// `self.is_zero()` branch fetches it again), so it never occupies registers across the formula.
+// ark add_assign_mixed: p += (x2, y2) for a finite affine (x2, y2) that `load(x2, y2)` delivers
+// (normalized, v <= 2 — or, for the G1 test's second ladder, a ladder state: limbs < 2^30). The
+// base point is fetched inside and dies after U2 / S2 (the rare `self.is_zero()` branch fetches it
+// again), so it never occupies registers across the formula.
 // In: X, Y limbs < 2^30, values <= 40; Z normalized. Out: normalized, values <= 64.
 template <typename F, typename Load>
 KZG_DEV void jac_madd(jac<F>& p, Load&& load) {
@@ -167,61 +168,6 @@ KZG_DEV void jac_madd(jac<F>& p, Load&& load) {
   p.x = t;
 }
 
-// p += q, both Jacobian (add-2007-bl) with the O / equal-point cases handled. Cold (10 per G1
-// point). In: p from jac_dbl<fp> (X, Y < 2^30), q normalized; values <= 64. Out normalized.
-template <typename F>
-KZG_DEV void jac_add(jac<F>& p, const jac<F>& q) {
-  const bool pzero = f_is_zero(p.z);
-  const bool qzero = f_is_zero(q.z);
-  F z1z1, z2z2, u1, s1, h, r;
-  f_sqr(z1z1, p.z);
-  f_sqr(z2z2, q.z);
-  f_mul(u1, p.x, z2z2);        // U1
-  f_mul(s1, p.y, q.z);
-  f_mul(s1, s1, z2z2);         // S1
-  f_mul(h, q.x, z1z1);
-  f_subk(h, h, u1, BlsFp::KB_8_28);
-  f_norm(h, h);                // H = U2 - U1
-  f_mul(r, q.y, p.z);
-  f_mul(r, r, z1z1);
-  f_subk(r, r, s1, BlsFp::KB_8_28);
-  f_norm(r, r);                // r' = S2 - S1
-  const bool same = !pzero && !qzero && f_is_zero(h) && f_is_zero(r);
-  if (__builtin_expect(pzero || qzero || same, 0)) {
-    if (same)
-      jac_dbl(p);
-    else if (pzero)
-      p = q;
-    return;
-  }
-  f_shl<1>(z1z1, p.z);
-  f_norm(z1z1, z1z1);
-  f_mul(z1z1, z1z1, q.z);
-  f_mul(p.z, z1z1, h);         // Z3 = 2 Z1 Z2 H
-  f_shl<1>(z1z1, h);
-  f_norm(z1z1, z1z1);
-  f_sqr(z1z1, z1z1);           // I = (2H)^2
-  f_mul(z2z2, h, z1z1);        // J = H I
-  f_mul(u1, u1, z1z1);         // V = U1 I
-  f_sqr(h, r);
-  f_shl<2>(h, h);              // r^2 = 4 r'^2
-  f_subk(h, h, z2z2, BlsFp::KB_8_28);
-  f_shl<1>(z1z1, u1);
-  f_subk(h, h, z1z1, BlsFp::KB_64_29);
-  f_norm(h, h);                // X3 = r^2 - J - 2V
-  f_subk(u1, u1, h, BlsFp::KB_128_28);
-  f_norm(u1, u1);              // V - X3
-  f_shl<1>(r, r);
-  f_norm(r, r);
-  f_mul(u1, r, u1);            // r (V - X3)
-  f_shl<1>(s1, s1);
-  f_norm(s1, s1);
-  f_mul(s1, s1, z2z2);         // 2 S1 J
-  f_subk(p.y, u1, s1, BlsFp::KB_8_28);
-  f_norm(p.y, p.y);            // Y3
-  p.x = h;
-}
-
 // [|u|] B for the affine finite base B delivered by load(x, y): 63 doublings, 5 mixed additions.
 template <typename F, typename Load>
 KZG_DEV void mul_abs_u_affine(jac<F>& acc, Load&& load) {
@@ -233,17 +179,6 @@ KZG_DEV void mul_abs_u_affine(jac<F>& acc, Load&& load) {
     if ((BLS_ABS_U >> b) & 1) jac_madd(acc, load);
   }
 }
-// [|u|] q for Jacobian q
-template <typename F>
-KZG_DEV void mul_abs_u_jac(jac<F>& acc, const jac<F>& q) {
-  acc = q;
-#pragma unroll 1
-  for (int b = BLS_ABS_U_BITS - 2; b >= 0; b--) {
-    jac_dbl(acc);
-    if ((BLS_ABS_U >> b) & 1) jac_add(acc, q);
-  }
-}
-
 // Jacobian (X, Y, Z) == affine (x, y)?  (X == x Z^2, Y == y Z^3, Z != 0). X, Y limbs < 2^30.
 template <typename F>
 KZG_DEV bool jac_eq_affine(const jac<F>& p, const F& x, const F& y) {
@@ -275,13 +210,24 @@ KZG_DEV bool in_subgroup_ref(Load&& load) {
 }
 
 // G1: P in G1  <=>  [u^2] P == -phi(P) = (BETA x, -y)   (u^2 = |u|^2)
-template <typename Load>
-KZG_DEV bool in_subgroup_fast_g1(Load&& load) {
+// The second [|u|] runs on the isomorphic curve E': y^2 = x^3 + Z^6 b, iota(x, y) = (Z^2 x, Z^3 y),
+// on which Q1 = [|u|] P = (X : Y : Z) is the AFFINE point (X, Y): a = 0 and neither formula reads
+// b, so its 5 additions are mixed additions (8M + 3S) instead of Jacobian ones (12M + 4S), and
+// [|u|] iota(Q1) = (X' : Y' : Z') is (X' : Y' : Z' Z) on E. Q1 = O (Z = 0) still ends in O.
+// park(q1) stores Q1; load_q(x, y) / load_qz(z) fetch it back (the kernel parks it in LDS).
+template <typename Load, typename Park, typename LoadQ, typename LoadQZ>
+KZG_DEV bool in_subgroup_fast_g1(Load&& load, Park&& park, LoadQ&& load_q, LoadQZ&& load_qz) {
   jac<fp> q2;
   {
     jac<fp> q1;
     mul_abs_u_affine(q1, load);
-    mul_abs_u_jac(q2, q1);
+    park(q1);
+  }
+  mul_abs_u_affine(q2, load_q);
+  {
+    fp z;
+    load_qz(z);
+    fp_mul(q2.z, q2.z, z);
   }
   fp x, y, beta;
   load(x, y);

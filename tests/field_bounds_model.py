@@ -347,42 +347,6 @@ def jac_madd(F, X, Y, Z, x2, y2):
     return jn(jn(t, xd), x2), jn(jn(y3, yd), y2), jn(jn(z3, zd), one)
 
 
-def jac_add(F, X1, Y1, Z1, X2, Y2, Z2):
-    F.canon_ok(Z1), F.canon_ok(Z2)
-    z1z1 = F.sqr(Z1, "Z1Z1")
-    z2z2 = F.sqr(Z2, "Z2Z2")
-    u1 = F.mul(X1, z2z2, "U1")
-    s1 = F.mul(Y1, Z2, "Y1Z2")
-    s1 = F.mul(s1, z2z2, "S1")
-    h = F.mul(X2, z1z1, "U2")
-    h = F.norm(F.subk(h, u1, "KB_8_28", "H"))
-    r = F.mul(Y2, Z1, "Y2Z1")
-    r = F.mul(r, z1z1, "S2")
-    r = F.norm(F.subk(r, s1, "KB_8_28", "r'"))
-    F.canon_ok(h), F.canon_ok(r)
-    xd, yd, zd = jac_dbl(F, X1, Y1, Z1)
-    z1z1 = F.norm(F.shl(Z1, 1))
-    z1z1 = F.mul(z1z1, Z2, "2Z1Z2")
-    z3 = F.mul(z1z1, h, "Z3")
-    z1z1 = F.norm(F.shl(h, 1))
-    z1z1 = F.sqr(z1z1, "I")
-    z2z2 = F.mul(h, z1z1, "J")
-    u1 = F.mul(u1, z1z1, "V")
-    h = F.sqr(r, "r'^2")
-    h = F.shl(h, 2)
-    h = F.subk(h, z2z2, "KB_8_28", "X3a")
-    z1z1 = F.shl(u1, 1)
-    h = F.norm(F.subk(h, z1z1, "KB_64_29", "X3"))
-    u1 = F.norm(F.subk(u1, h, "KB_128_28", "V-X3"))
-    r = F.norm(F.shl(r, 1))
-    u1 = F.mul(r, u1, "r(V-X3)")
-    s1 = F.norm(F.shl(s1, 1))
-    s1 = F.mul(s1, z2z2, "2S1J")
-    y3 = F.norm(F.subk(u1, s1, "KB_8_28", "Y3"))
-    jn = (lambda a, b: V2(vmax(a.c0, b.c0), vmax(a.c1, b.c1))) if F.two else vmax
-    return jn(jn(h, xd), X2), jn(jn(y3, yd), Y2), jn(jn(z3, zd), Z2)
-
-
 def jac_eq_affine(F, X, Y, Z, x, y):
     z2 = F.sqr(Z, "z2")
     t = F.mul(x, z2, "xZ2")
@@ -419,23 +383,16 @@ def _within(F, a, b):
     return all(all(x <= y for x, y in zip(u.limbs, w.limbs)) and u.val <= w.val for u, w in pairs)
 
 
-def ladder_invariant(F, base_x, base_y, add_base=None, rounds=12):
+def ladder_invariant(F, base_x, base_y, rounds=12):
     """A bound set S for the ladder accumulator (X, Y, Z) that contains the starting point and is
-    CLOSED under one ladder step (dbl, then optionally madd(base) or add(add_base)) — hence bounds
-    every state reached by mul_abs_u_affine / mul_abs_u_jac / in_subgroup_ref for any input.
-    Found by joined iteration, then inflated and verified closed."""
-    if add_base is None:
-        X, Y, Z = base_x, base_y, F.one()
-    else:
-        X, Y, Z = add_base
+    CLOSED under one ladder step (dbl, then optionally madd(base)) — hence bounds every state
+    reached by mul_abs_u_affine / in_subgroup_ref for any input. Found by joined iteration, then
+    inflated and verified closed."""
+    X, Y, Z = base_x, base_y, F.one()
 
     def step(X, Y, Z):
         x1, y1, z1 = jac_dbl(F, X, Y, Z)
-        outs = [(x1, y1, z1)]
-        if add_base is None:
-            outs.append(jac_madd(F, x1, y1, z1, base_x, base_y))
-        else:
-            outs.append(jac_add(F, x1, y1, z1, *add_base))
+        outs = [(x1, y1, z1), jac_madd(F, x1, y1, z1, base_x, base_y)]
         nx, ny, nz = X, Y, Z
         for ox, oy, oz in outs:
             nx, ny, nz = join(F, nx, ox), join(F, ny, oy), join(F, nz, oz)

@@ -18,10 +18,13 @@ def test_ladders_closed(two):
         M.normalized(Fraction(101, 100))
     S1 = M.ladder_invariant(F, base, base)                     # mul_abs_u_affine / in_subgroup_ref
     if not two:
-        S2 = M.ladder_invariant(F, base, base, add_base=S1)    # mul_abs_u_jac (G1 second ladder)
+        # G1 second ladder: Q1 = S1's (X, Y) is the affine base on the isomorphic curve; the
+        # result's Z is multiplied by Q1's Z before the comparison (curve.hpp in_subgroup_fast_g1)
+        S2 = M.ladder_invariant(F, S1[0], S1[1])
+        z = M.mul(S2[2], S1[2], "Z'Z")
         beta_x = M.mul(base, M.normalized(1))
         ny = M.norm(M.subk(M.normalized(0), base, "KB_64_31"))
-        M.jac_eq_affine(F, *S2, beta_x, ny)
+        M.jac_eq_affine(F, S2[0], S2[1], z, beta_x, ny)
     M.jac_eq_affine(F, *S1, base, base)
 
 
