@@ -339,13 +339,25 @@ KZG_DEV void fp_from_mont(Fe<Tr>& canon, const Fe<Tr>& a) {
 // from 162 to 88 VGPRs).
 template <class Tr>
 KZG_DEV void fp_pow_pm3d4(Fe<Tr>& r, const Fe<Tr>& a) {
-  Fe<Tr> tab[Tr::SQRT_TABLE];
-  Fe<Tr> a2;
+  static_assert(Tr::SQRT_TABLE == 8, "table held as one 8-wide register vector per limb");
+  typedef uint32_t v8u __attribute__((ext_vector_type(8)));
+  // tab[k][e] = limb k of a^(2e+1): a wave-uniform (SGPR) index into a register vector becomes
+  // one m0-indexed v_movrels_b32 per limb — 14 moves per lookup, no memory traffic (a scratch
+  // table costs ~1.4 KB of HBM re-reads per point once the per-CU working set exceeds L2).
+  v8u tab[Tr::NL];
+  Fe<Tr> a2, t = a;
   fp_sqr(a2, a);
-  tab[0] = a;
+#pragma unroll
+  for (int k = 0; k < Tr::NL; k++) tab[k][0] = a.v[k];
 #pragma clang loop unroll(full)
-  for (int k = 1; k < Tr::SQRT_TABLE; k++) fp_mul(tab[k], tab[k - 1], a2);
-  Fe<Tr> acc = tab[Tr::SQRT_STEP_IDX[0]];
+  for (int e = 1; e < Tr::SQRT_TABLE; e++) {
+    fp_mul(t, t, a2);
+#pragma unroll
+    for (int k = 0; k < Tr::NL; k++) tab[k][e] = t.v[k];
+  }
+  Fe<Tr> acc;
+#pragma unroll
+  for (int k = 0; k < Tr::NL; k++) acc.v[k] = tab[k][Tr::SQRT_STEP_IDX[0]];
 #pragma unroll 1
   for (int s = 1; s < Tr::SQRT_STEPS; s++) {
     const int nsq = __builtin_amdgcn_readfirstlane(Tr::SQRT_STEP_SQ[s]);
@@ -353,7 +365,8 @@ KZG_DEV void fp_pow_pm3d4(Fe<Tr>& r, const Fe<Tr>& a) {
 #pragma unroll 1
     for (int k = 0; k < nsq; k++) fp_sqr(acc, acc);
     if (idx >= 0) {
-      const Fe<Tr> t = tab[idx];  // wave-uniform index: register-indexed move (v_movrels)
+#pragma unroll
+      for (int k = 0; k < Tr::NL; k++) t.v[k] = tab[k][idx];
       fp_mul(acc, acc, t);
     }
   }
