@@ -31,8 +31,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "kzg-setup-powersoftau_amd"))
 
 HBM_PEAK_GBS = 8000.0           # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-FP_MUL_PEAK = 77.7e9            # measured radix-2^28 Montgomery multiplies/s (best variant), profiles/r01_mont28_microbench.txt
-FP_MUL_PER_G1 = 1510            # Fp multiplies per G1 point on the fast path
+# integer-VALU issue roof: 256 CUs x 4 SIMDs, one wave64 VALU instruction per 4 cycles per SIMD
+# (16 lanes) at the 2.4 GHz peak engine clock = 614.4 G wave-instructions/s (MI355X_MICROARCH.md)
+VALU_PEAK_WAVE_INSTR = 256 * 4 * 2.4e9 / 4
 ALG_BYTES_G1 = 144              # 48 B read + 96 B written per G1 point
 ALG_BYTES_G2 = 288
 
@@ -83,16 +84,35 @@ def cpu_baseline(comp1, comp2, sample_log2):
     }
 
 
-def pmc_traffic(n_g1_local):
-    """HBM bytes per G1 codec launch from the committed rocprofv3 PMC pass, if present."""
+def pmc_profile():
+    """The committed rocprofv3 PMC summary (tools/pmc_summary.py -> profiles/pmc_traffic.json)."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if not os.path.exists(path):
-        return None
     try:
-        d = json.load(open(path))
-        return d["g1_bytes_per_point"] * n_g1_local
-    except Exception:
+        return json.load(open(path))
+    except (OSError, ValueError):
         return None
+
+
+def pmc_traffic(pmc, n_g1_local):
+    """HBM bytes per G1 codec launch (decompress + check) from the PMC FETCH/WRITE passes."""
+    try:
+        return pmc["g1_bytes_per_point"] * n_g1_local
+    except (TypeError, KeyError):
+        return None
+
+
+def valu_roofline(pmc, n_g1_local, g1_ms):
+    """Integer-VALU roof of the G1 codec: PMC SQ_INSTS_VALU per wave (= the instruction stream one
+    lane runs for its point) x waves per launch / the event-timed launch time, against the issue
+    peak. This, not HBM, is the roof that binds."""
+    try:
+        per_pt = sum(pmc["kernels"][k]["valu_insts_per_wave"] for k in ("k_g1_decompress", "k_g1_check"))
+    except (TypeError, KeyError):
+        return None
+    achieved = per_pt * (n_g1_local / 64) / (g1_ms * 1e-3)
+    return {"valu_instr_per_g1_point": per_pt, "achieved_wave_instr_per_s": achieved,
+            "peak_wave_instr_per_s": VALU_PEAK_WAVE_INSTR, "frac": achieved / VALU_PEAK_WAVE_INSTR,
+            "source": "instruction counts: profiles/pmc_traffic.json (SQ_INSTS_VALU); time: this run"}
 
 
 def e2e_preprocess(n_log2, seed, dev, kzgpot, D):
@@ -281,7 +301,8 @@ def main():
     result = None
     if rank == 0:
         achieved = ALG_BYTES_G1 * m1 / (g1_ms * 1e-3) / 1e9
-        traffic = pmc_traffic(m1)
+        pmc = pmc_profile()
+        traffic = pmc_traffic(pmc, m1)
         result = {
             "metric": "G1+G2 points decompressed+checked/sec, 2^27 BLS12-381 PoT",
             "value": value,
@@ -314,12 +335,7 @@ def main():
                 "algorithmic_bytes_per_point": ALG_BYTES_G1,
                 "note": "integer-VALU bound, not HBM: see valu",
             },
-            "valu": {
-                "fp_mul_per_g1_point": FP_MUL_PER_G1,
-                "achieved_fp_mul_per_s": FP_MUL_PER_G1 * m1 / (g1_ms * 1e-3),
-                "peak_fp_mul_per_s": FP_MUL_PEAK,
-                "frac": FP_MUL_PER_G1 * m1 / (g1_ms * 1e-3) / FP_MUL_PEAK,
-            },
+            "valu": valu_roofline(pmc, m1, g1_ms),
             "kernels_ms": {"g1_codec": g1_ms, "g2_codec": g2_ms},
             "verified_bit_exact": verified,
             "rejected_points": 0 if bad == KD.NO_BAD else 1,
