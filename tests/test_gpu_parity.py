@@ -276,3 +276,4 @@ def test_bn254_synth_round_trip(gpu):
     for i in random.Random(3).sample(range(n), 64):
         st, want = O.bn254_g1_decompress_point(c[32 * i:32 * i + 32])
         assert st == 0 and want == o[64 * i:64 * i + 64]
+

@@ -99,3 +99,26 @@ def test_python_mirror_api_surface(kzgpot_mod):
                  "g1_decompress", "g2_decompress", "blake2b_hex", "KZG_SETUP_FILE", "KZG_SETUP_FILE_DIGEST",
                  "FASTKZG_SETUP_FILE_DIGEST", "POWERSOFTAU_DIGEST", "TAU_POWERS_LENGTH"):
         assert hasattr(kzgpot_mod, name), name
+
+
+CLI = {m: os.path.join(PKG, "build", f"kzgpot-preprocess-{m}") for m in ("kgz", "fastkgz")}
+
+
+@pytest.mark.parametrize("mode", ["kgz", "fastkgz"])
+def test_cli_reference_failure_paths(mode, tmp_path):
+    """The native drop-ins for src/bin/preprocess-{kgz,fastkgz}: --help, and the reference's
+    panics (exit 101) for a missing ./powersoftau (no download here) and a wrong-size transcript
+    (preprocess-kgz.rs:83-91) — both decided before any GPU work."""
+    exe = CLI[mode]
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-C", PKG, "-j", "8"], check=True)
+    r = subprocess.run([exe, "--help"], capture_output=True, text=True)
+    assert r.returncode == 0 and "--transcript" in r.stdout
+    r = subprocess.run([exe], cwd=tmp_path, capture_output=True, text=True)
+    assert r.returncode == 101 and "`powersoftau` not found" in r.stderr
+    bad = tmp_path / "powersoftau"
+    bad.write_bytes(b"\0" * 1000)
+    r = subprocess.run([exe, "--n-log2", "10"], cwd=tmp_path, capture_output=True, text=True)
+    assert r.returncode == 101
+    assert "The size of `powersoftau` should be 296176, but it's 1000, so something isn't right." in r.stderr
+    assert not (tmp_path / "kzg_setup").exists()
