@@ -47,6 +47,9 @@ def parse():
     ap.add_argument("--g2-log2", type=int, default=16)
     ap.add_argument("--seed", type=int, default=0x5EED)
     ap.add_argument("--no-gather", action="store_true", help="skip the RCCL all-gather (N > 1)")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL, the product path) or gloo (rehearsal)")
+    ap.add_argument("--gather-chunks", type=int, default=4,
+                    help="N > 1: G1 chunks per rank; each chunk's all-gather overlaps the next chunk's decode")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-log2", type=int, default=15)
@@ -159,48 +162,95 @@ def main():
     import torch
     import torch.distributed as dist
 
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # one process per GPU; ranks beyond the visible GPUs wrap around (a gloo rehearsal of the N > 1
+    # path on a one-GPU box: --dist-backend gloo)
+    dev = torch.device("cuda", local_rank % max(1, torch.cuda.device_count()))
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.dist_backend)
 
     import kzgpot
     from kzgpot import device as D
     from kzgpot import dist as KD
 
     n1, n2 = 1 << args.g1_log2, 1 << args.g2_log2
-    lo1, hi1 = KD.shard_bounds(n1, rank, world)
-    lo2, hi2 = KD.shard_bounds(n2, rank, world)
-    m1, m2 = hi1 - lo1, hi2 - lo2
+    gather = world > 1 and not args.no_gather
+    # Which points this rank decodes, as (global start, count) blocks. N > 1 with the gather:
+    # block-cyclic (kzgpot/dist.py) — G1 in `--gather-chunks` chunks whose all-gathers overlap the
+    # next chunk's decoding, G2 (2^16 points) in one. Otherwise one contiguous shard per rank.
+    if gather:
+        ch1 = args.gather_chunks
+        b1, b2 = KD.cyclic_block(n1, world, ch1), KD.cyclic_block(n2, world, 1)
+        blocks1 = [(g, b1) for g in KD.owned_block_starts(n1, rank, world, ch1)]
+        blocks2 = [(g, b2) for g in KD.owned_block_starts(n2, rank, world, 1)]
+    else:
+        lo1, hi1 = KD.shard_bounds(n1, rank, world)
+        lo2, hi2 = KD.shard_bounds(n2, rank, world)
+        blocks1, blocks2 = [(lo1, hi1 - lo1)], [(lo2, hi2 - lo2)]
+    m1, m2 = sum(c for _, c in blocks1), sum(c for _, c in blocks2)
+
+    def synth(kind, seed, blocks):
+        parts = [D.synth(kind, seed, g, c, dev, with_expected=not args.no_verify) for g, c in blocks]
+        comp = torch.cat([p[0] for p in parts]) if len(parts) > 1 else parts[0][0]
+        return comp, [p[1] for p in parts]
 
     t_gen = time.perf_counter()
-    comp1, exp1 = D.synth("g1", args.seed, lo1, m1, dev, with_expected=not args.no_verify)
-    comp2, exp2 = D.synth("g2", args.seed + 1, lo2, m2, dev, with_expected=not args.no_verify)
+    comp1, exp1 = synth("g1", args.seed, blocks1)
+    comp2, exp2 = synth("g2", args.seed + 1, blocks2)
     torch.cuda.synchronize()
     t_gen = time.perf_counter() - t_gen
-    out1 = torch.empty(m1 * 96, dtype=torch.uint8, device=dev)
-    out2 = torch.empty(m2 * 192, dtype=torch.uint8, device=dev)
-    key1 = torch.empty(1, dtype=torch.int64, device=dev)
-    key2 = torch.empty(1, dtype=torch.int64, device=dev)
-    gather = world > 1 and not args.no_gather
+    # outputs: the full contiguous arkworks buffers (gather) or this rank's shard
+    out1 = torch.empty((n1 if gather else m1) * 96, dtype=torch.uint8, device=dev)
+    out2 = torch.empty((n2 if gather else m2) * 192, dtype=torch.uint8, device=dev)
+    keys1 = torch.empty(len(blocks1), dtype=torch.int64, device=dev)  # one first-bad key per launch
+    keys2 = torch.empty(len(blocks2), dtype=torch.int64, device=dev)
+
+    def dst_of(out, blocks, c, rec):
+        """Where block c of this rank lands in `out`."""
+        g0, cnt = blocks[c]
+        off = g0 if gather else sum(x for _, x in blocks[:c])
+        return out[off * rec:(off + cnt) * rec]
 
     ev = []
 
     def step(record):
-        if record:
-            e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
-            e[0].record()
-        D.codec_dev("g1_decompress", comp1, out1, key1)
-        if record:
-            e[1].record()
-        D.codec_dev("g2_decompress", comp2, out2, key2)
-        if record:
-            e[2].record()
-            ev.append(e)
-        full = None
+        marks = []
+
+        def launch(op, comp, blocks, rin, out, rout, keys, c):
+            cnt = blocks[c][1]
+            src = comp[sum(x for _, x in blocks[:c]) * rin:][:cnt * rin]
+            e = [torch.cuda.Event(enable_timing=True) for _ in range(2)] if record else None
+            if record:
+                e[0].record()
+            D.codec_dev(op, src, dst_of(out, blocks, c, rout), keys[c:c + 1])
+            if record:
+                e[1].record()
+                marks.append((op, e))
+
         if gather:
-            full = (KD.gather_shards(out1, world), KD.gather_shards(out2, world))
-        return full
+            works = KD.decode_gather_pipelined(
+                lambda c, g0, dst: launch("g1_decompress", comp1, blocks1, 48, out1, 96, keys1, c),
+                out1, 96, n1, rank, world, len(blocks1))
+            works += KD.decode_gather_pipelined(
+                lambda c, g0, dst: launch("g2_decompress", comp2, blocks2, 96, out2, 192, keys2, c),
+                out2, 192, n2, rank, world, len(blocks2))
+            for w in works:
+                w.wait()  # the current stream waits for the collectives
+        else:
+            for c in range(len(blocks1)):
+                launch("g1_decompress", comp1, blocks1, 48, out1, 96, keys1, c)
+            for c in range(len(blocks2)):
+                launch("g2_decompress", comp2, blocks2, 96, out2, 192, keys2, c)
+        if record:
+            ev.append(marks)
+
+    def bad_key():
+        ks = [KD.key_with_offset(D.read_key(keys1[c:c + 1]), blocks1[c][0]) for c in range(len(blocks1))]
+        ks += [KD.key_with_offset(D.read_key(keys2[c:c + 1]), blocks2[c][0]) for c in range(len(blocks2))]
+        return min(ks)
 
     for _ in range(args.warmup):
         step(False)
@@ -208,13 +258,23 @@ def main():
 
     verified = None
     if not args.no_verify:
-        k = KD.key_with_offset(D.read_key(key1), lo1), KD.key_with_offset(D.read_key(key2), lo2)
-        ok = k[0] == KD.NO_BAD and k[1] == KD.NO_BAD
-        ok = ok and torch.equal(out1, exp1) and torch.equal(out2, exp2)
-        if gather:
-            full1, full2 = step(False)
+        if args.warmup == 0:
+            step(False)
             torch.cuda.synchronize()
-            ok = ok and torch.equal(full1[lo1 * 96: hi1 * 96], exp1) and torch.equal(full2[lo2 * 192: hi2 * 192], exp2)
+        ok = bad_key() == KD.NO_BAD
+        for out, blocks, exps, rec in ((out1, blocks1, exp1, 96), (out2, blocks2, exp2, 192)):
+            for c, e in enumerate(exps):
+                ok = ok and torch.equal(dst_of(out, blocks, c, rec), e)
+            if gather:  # blocks decoded by the other ranks: per-block checksums against their owners'
+                nb = out.numel() // (blocks[0][1] * rec)
+                mine = torch.zeros(nb, 2, dtype=torch.int64, device=dev)
+                w = torch.arange(1, blocks[0][1] * rec // 8 + 1, dtype=torch.int64, device=dev)
+                for (g0, cnt), e in zip(blocks, exps):
+                    v = e.view(torch.int64)
+                    mine[g0 // cnt] = torch.stack([v.sum(), (v * w).sum()])
+                dist.all_reduce(mine)  # each block has exactly one owner
+                got = out.view(torch.int64).view(nb, -1)
+                ok = ok and torch.equal(torch.stack([got.sum(1), (got * w).sum(1)], 1), mine)
         if world > 1:
             t = torch.tensor([1 if ok else 0], device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MIN)
@@ -236,10 +296,9 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        bad = KD.allreduce_min_key(min(KD.key_with_offset(D.read_key(key1), lo1),
-                                       KD.key_with_offset(D.read_key(key2), lo2)), dev)
+        bad = KD.allreduce_min_key(bad_key(), dev)
     else:
-        bad = min(D.read_key(key1), D.read_key(key2))
+        bad = bad_key()
 
     # SURVEY §8f row 2 (loader mirror), measured after the timed region on rank 0: the G1 ark
     # records just produced -> in-memory GroupAffine (deserialize_unchecked), HBM-bound.
@@ -247,11 +306,12 @@ def main():
     if rank == 0 and not args.no_next_rows:
         outl = torch.empty(m1 * 104, dtype=torch.uint8, device=dev)
         keyl = torch.empty(1, dtype=torch.int64, device=dev)
-        D.codec_dev("g1_load", out1, outl, keyl)
+        rec1 = out1[:m1 * 96]  # m1 G1 ark records (any of them: all decoded and verified)
+        D.codec_dev("g1_load", rec1, outl, keyl)
         le = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         le[0].record()
         for _ in range(5):
-            D.codec_dev("g1_load", out1, outl, keyl)
+            D.codec_dev("g1_load", rec1, outl, keyl)
         le[1].record()
         torch.cuda.synchronize()
         load_ms = le[0].elapsed_time(le[1]) / 5
@@ -293,8 +353,8 @@ def main():
         if world == 1 and args.e2e_log2 > 0:
             next_rows.update(e2e_preprocess(args.e2e_log2, args.seed + 3, dev, kzgpot, D))
 
-    g1_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / len(ev)
-    g2_ms = sum(e[1].elapsed_time(e[2]) for e in ev) / len(ev)
+    g1_ms = sum(e[0].elapsed_time(e[1]) for marks in ev for op, e in marks if op == "g1_decompress") / len(ev)
+    g2_ms = sum(e[0].elapsed_time(e[1]) for marks in ev for op, e in marks if op == "g2_decompress") / len(ev)
     ms_per_step = elapsed * 1e3 / args.steps
     value = (n1 + n2) * args.steps / elapsed
 
@@ -319,7 +379,8 @@ def main():
             "config": {
                 "workload": f"config 4: 2^{args.g1_log2} G1 + 2^{args.g2_log2} G2 compressed BLS12-381 "
                             "points -> arkworks uncompressed, subgroup-checked"
-                            + (", RCCL all-gather to one contiguous buffer" if gather else ""),
+                            + (f", block-cyclic shards, RCCL all-gather to one contiguous buffer pipelined in "
+                               f"{args.gather_chunks} chunks" if gather else ""),
                 "g1_points": n1, "g2_points": n2, "parallelism": f"shard{world}",
                 "subgroup_test": "endomorphism (phi/psi), bit-exact accept/reject vs ark mul_bits(r)",
             },

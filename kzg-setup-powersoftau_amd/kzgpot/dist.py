@@ -1,9 +1,18 @@
 """Multi-GPU sharding for the point codec: one process per GPU (torch.distributed over RCCL).
 
-The τ^i arrays shard trivially (every point is independent). Each rank decodes one contiguous,
-equal-sized shard of every section; the only exchange is the final all-gather that assembles one
-contiguous arkworks buffer on every rank (the north_star's "final RCCL all-gather over xGMI"),
-plus an 8-byte all-reduce(min) of the first-bad key. No other communication.
+The τ^i arrays shard trivially (every point is independent); the only exchange is the all-gather
+that assembles one contiguous arkworks buffer on every rank (the north_star's "final RCCL
+all-gather over xGMI"), plus an 8-byte all-reduce(min) of the first-bad key.
+
+Two layouts:
+  * contiguous shards (`shard_bounds` + `gather_shards`): rank r decodes [r n/N, (r+1) n/N), one
+    all-gather at the end;
+  * block-cyclic, pipelined (`cyclic_block` + `decode_gather_pipelined`): the n points are cut
+    into N x C equal blocks and rank r owns blocks c N + r (c < C). Chunk c's N blocks are
+    adjacent in the output, so its all-gather is ONE in-place `all_gather_into_tensor` into a
+    contiguous slice of the final buffer — issued asynchronously right after the rank's chunk-c
+    launch, so the xGMI transfer of chunk c overlaps the decoding of chunk c + 1 and only the
+    last chunk's gather is exposed.
 
 These helpers are backend-agnostic so the same code is exercised with `gloo` on CPU tensors in
 tests/test_dist.py and with `nccl` (= RCCL on ROCm) on HBM tensors in bench.py.
@@ -33,6 +42,41 @@ def gather_shards(local: torch.Tensor, world: int, group=None) -> torch.Tensor:
         return out
     dist.all_gather_into_tensor(out, local, group=group)
     return out
+
+
+def cyclic_block(n: int, world: int, chunks: int) -> int:
+    """Block size of the block-cyclic layout (n must split into world x chunks equal blocks)."""
+    if n % (world * chunks):
+        raise ValueError(f"{n} points do not split into {world} x {chunks} equal blocks")
+    return n // (world * chunks)
+
+
+def owned_block_starts(n: int, rank: int, world: int, chunks: int) -> list[int]:
+    """First global point index of each block rank owns, in chunk order (block c N + rank)."""
+    b = cyclic_block(n, world, chunks)
+    return [(c * world + rank) * b for c in range(chunks)]
+
+
+def decode_gather_pipelined(decode, full: torch.Tensor, rec_out: int, n: int, rank: int, world: int,
+                            chunks: int, group=None) -> list:
+    """For c = 0..chunks-1: `decode(c, g0, dst)` writes the rank's chunk-c block (global points
+    [g0, g0 + B)) into its final place `dst` inside `full` (n records of rec_out bytes), then the
+    chunk's N blocks are all-gathered in place, asynchronously. Returns the work handles: wait on
+    them (on GPU this orders the current stream after the collectives) before reading `full`."""
+    b = cyclic_block(n, world, chunks)
+    works = []
+    for c in range(chunks):
+        g0 = (c * world + rank) * b
+        mine = full[g0 * rec_out:(g0 + b) * rec_out]
+        decode(c, g0, mine)
+        if world == 1:
+            continue
+        region = full[c * world * b * rec_out:(c + 1) * world * b * rec_out]
+        if dist.get_backend(group) == "gloo":  # no all_gather_into_tensor; output views alias `full`
+            works.append(dist.all_gather(list(region.chunk(world)), mine.clone(), group=group, async_op=True))
+        else:
+            works.append(dist.all_gather_into_tensor(region, mine, group=group, async_op=True))
+    return works
 
 
 def key_with_offset(key: int, offset: int) -> int:

@@ -86,3 +86,79 @@ def test_shard_bounds_cover():
                 assert b == c and a <= b
     assert KD.key_with_offset(KD.NO_BAD, 5) == KD.NO_BAD
     assert KD.key_with_offset((3 << 8) | 5, 100) == (103 << 8) | 5
+
+
+def _worker_pipelined(rank, world, port, data, n, chunks, q):
+    import sys
+
+    sys.path.insert(0, os.path.join(ROOT, "kzg-setup-powersoftau_amd"))
+    from kzgpot import dist as KD
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "_build", "libkzgpot_oracle.so"))
+    full = torch.zeros(n * 96, dtype=torch.uint8)
+    keys = []
+
+    def decode(c, g0, dst):  # the C oracle stands in for the chunk-c kernel launch
+        b = dst.numel() // 96
+        out = ctypes.create_string_buffer(b * 96)
+        fb = ctypes.c_int64(-1)
+        r = lib.oracle_g1_decompress(data[g0 * 48:(g0 + b) * 48], ctypes.c_size_t(b), out, 0, ctypes.byref(fb),
+                                     None, 1, 1)
+        dst.copy_(torch.frombuffer(bytearray(out.raw), dtype=torch.uint8))
+        keys.append(KD.key_with_offset(KD.NO_BAD if r == 0 else ((fb.value << 8) | (-r)), g0))
+
+    works = KD.decode_gather_pipelined(decode, full, 96, n, rank, world, chunks)
+    for w in works:
+        w.wait()
+    gkey = KD.allreduce_min_key(min(keys), "cpu")
+    q.put((rank, bytes(full.numpy()), gkey))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,chunks", [(2, 4), (4, 2)])
+def test_block_cyclic_pipelined_gather(oracle_lib, world, chunks):
+    """bench.py's N > 1 layout: rank r decodes blocks c N + r and all-gathers each chunk in place
+    as soon as it is decoded; every rank ends with the single-process buffer and the global
+    first-bad key (a bad point planted in a block of the last rank)."""
+    vecs = [v for v in golden("g1_decompress") if v["check"] and v["status"] == 0][:32]
+    bad_vec = next(v for v in golden("g1_decompress") if v["status"] == 5)
+    n = 32
+    data = bytearray(b"".join(bytes.fromhex(v["in"]) for v in vecs))
+    from kzgpot import dist as KD
+
+    b = KD.cyclic_block(n, world, chunks)
+    bad_index = KD.owned_block_starts(n, world - 1, world, chunks)[1] + b - 1
+    data[bad_index * 48:(bad_index + 1) * 48] = bytes.fromhex(bad_vec["in"])
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_pipelined, args=(r, world, port, bytes(data), n, chunks, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    out = ctypes.create_string_buffer(n * 96)
+    fb = ctypes.c_int64(-1)
+    r = oracle_lib.oracle_g1_decompress(bytes(data), ctypes.c_size_t(n), out, 0, ctypes.byref(fb), None, 1, 1)
+    assert r == -5 and fb.value == bad_index
+    for _, full, gkey in got:
+        assert full == out.raw
+        assert gkey == (bad_index << 8) | 5
+
+
+def test_cyclic_layout():
+    from kzgpot import dist as KD
+
+    n, world, chunks = 1 << 12, 8, 4
+    b = KD.cyclic_block(n, world, chunks)
+    starts = sorted(s for r in range(world) for s in KD.owned_block_starts(n, r, world, chunks))
+    assert starts == list(range(0, n, b))
+    with pytest.raises(ValueError):
+        KD.cyclic_block(100, 8, 4)
