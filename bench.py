@@ -322,6 +322,25 @@ def main():
             "achieved_GBs": load_gbs, "peak_GBs": HBM_PEAK_GBS, "hbm_frac": load_gbs / HBM_PEAK_GBS,
             "all_accepted": D.read_key(keyl) == KD.NO_BAD}}
         del outl
+        # SURVEY §8f row 3 (uncompressed-input mode, the read_g1 loop alone): pairing-uncompressed
+        # records = per-coordinate byte reversal of the ark records (A6 identity); decode them back
+        nt = min(m1, 1 << 24)
+        ark = rec1[:nt * 96]
+        pin = ark.view(nt, 2, 48).flip(-1).contiguous().view(-1)
+        outt = torch.empty(nt * 96, dtype=torch.uint8, device=dev)
+        keyt = torch.empty(1, dtype=torch.int64, device=dev)
+        D.codec_dev("g1_transcode", pin, outt, keyt)
+        te = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        te[0].record()
+        D.codec_dev("g1_transcode", pin, outt, keyt)
+        te[1].record()
+        torch.cuda.synchronize()
+        tr_ms = te[0].elapsed_time(te[1])
+        next_rows["g1_transcode_uncompressed"] = {
+            "kernel": "k_g1_check<PairingBE> (read_g1: flags, x/y < p, curve test, subgroup, ark emit)",
+            "points": nt, "launch_ms": tr_ms, "points_per_s": nt / (tr_ms * 1e-3), "algorithmic_bytes_per_point": 192,
+            "verified_bit_exact": bool(D.read_key(keyt) == KD.NO_BAD and torch.equal(outt, ark))}
+        del pin, outt
         # BN254 G1, ark compressed (32 B) -> uncompressed (64 B)
         if args.bn254_log2 > 0:
             nb = 1 << args.bn254_log2
