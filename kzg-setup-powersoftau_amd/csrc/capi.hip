@@ -33,15 +33,20 @@ constexpr uint64_t kNoBad = ~0ull;
     }                                                                                    \
   } while (0)
 
-// Per-device staging buffers for the host-buffer API (grown on demand, reused across calls).
-struct DevCtx {
-  std::mutex mu;
+// Per-device staging for the host-buffer API (grown on demand, reused across calls): two slots,
+// each with its own stream, so chunk k's kernel runs while the host thread moves chunk k-1's
+// output back and chunk k+1's input in (run_host).
+struct Slot {
   hipStream_t stream = nullptr;
   void* d_in = nullptr;
   void* d_out = nullptr;
   uint8_t* d_status = nullptr;
   unsigned long long* d_key = nullptr;
   size_t cap_in = 0, cap_out = 0, cap_status = 0;
+};
+struct DevCtx {
+  std::mutex mu;
+  Slot slot[2];
 };
 DevCtx g_ctx[64];
 
@@ -70,7 +75,10 @@ int decode_key(uint64_t key, int64_t* first_bad) {
   return -(int)(key & 0xff);
 }
 
-// Run one op over host buffers on device `dev`, in chunks that bound the staging memory.
+// Run one op over host buffers on device `dev`, in chunks that bound the staging memory. Chunks
+// alternate between two slots/streams: while the GPU decodes chunk k, this thread copies chunk
+// k-1's output out and chunk k+1's input in (pageable copies block the host, not the other
+// stream), so PCIe time hides behind the kernels except for the first input and last output.
 int run_host(int dev, CodecOp op, const uint8_t* in, size_t n, uint8_t* out, uint32_t flags, int64_t* first_bad,
              uint8_t* status) {
   if (first_bad) *first_bad = -1;
@@ -80,26 +88,39 @@ int run_host(int dev, CodecOp op, const uint8_t* in, size_t n, uint8_t* out, uin
   DevCtx& c = g_ctx[dev];
   std::lock_guard<std::mutex> lock(c.mu);
   HIP_TRY(hipSetDevice(dev));
-  if (!c.stream) HIP_TRY(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
   const uint64_t rin = in_record(op), rout = out_record(op);
-  const size_t chunk = std::min<size_t>(n, (size_t)1 << 22);
-  if (ensure(&c.d_in, &c.cap_in, chunk * rin)) return KZGPOT_E_DEVICE;
-  if (ensure(&c.d_out, &c.cap_out, chunk * rout)) return KZGPOT_E_DEVICE;
-  if (ensure((void**)&c.d_status, &c.cap_status, chunk)) return KZGPOT_E_DEVICE;
-  if (!c.d_key) HIP_TRY(hipMalloc(&c.d_key, sizeof(unsigned long long)));
-  uint64_t best = kNoBad;
-  for (size_t off = 0; off < n; off += chunk) {
-    const size_t m = std::min(chunk, n - off);
-    HIP_TRY(hipMemcpyAsync(c.d_in, in + off * rin, m * rin, hipMemcpyHostToDevice, c.stream));
-    HIP_TRY(hipMemsetAsync(c.d_key, 0xff, sizeof(unsigned long long), c.stream));
-    HIP_TRY(launch_codec(op, c.d_in, c.d_out, m, flags, c.d_key, status ? c.d_status : nullptr, c.stream));
-    HIP_TRY(hipMemcpyAsync(out + off * rout, c.d_out, m * rout, hipMemcpyDeviceToHost, c.stream));
-    if (status) HIP_TRY(hipMemcpyAsync(status + off, c.d_status, m, hipMemcpyDeviceToHost, c.stream));
-    unsigned long long key = kNoBad;
-    HIP_TRY(hipMemcpyAsync(&key, c.d_key, sizeof key, hipMemcpyDeviceToHost, c.stream));
-    HIP_TRY(hipStreamSynchronize(c.stream));
-    if (key != kNoBad && best == kNoBad) best = ((uint64_t)(key >> 8) + off) << 8 | (key & 0xff);
+  const size_t chunk = std::min<size_t>(n, (size_t)1 << 21);  // 2 x 2^21 x 288 B of staging at most
+  const size_t nchunks = (n + chunk - 1) / chunk;
+  for (int k = 0; k < (nchunks > 1 ? 2 : 1); k++) {
+    Slot& sl = c.slot[k];
+    if (!sl.stream) HIP_TRY(hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking));
+    if (ensure(&sl.d_in, &sl.cap_in, chunk * rin)) return KZGPOT_E_DEVICE;
+    if (ensure(&sl.d_out, &sl.cap_out, chunk * rout)) return KZGPOT_E_DEVICE;
+    if (status && ensure((void**)&sl.d_status, &sl.cap_status, chunk)) return KZGPOT_E_DEVICE;
+    if (!sl.d_key) HIP_TRY(hipMalloc(&sl.d_key, sizeof(unsigned long long)));
   }
+  uint64_t best = kNoBad;
+  // drain chunk j: its output (and status, key) back to the host
+  auto drain = [&](size_t j) -> int {
+    Slot& sl = c.slot[j & 1];
+    const size_t off = j * chunk, m = std::min(chunk, n - off);
+    HIP_TRY(hipMemcpyAsync(out + off * rout, sl.d_out, m * rout, hipMemcpyDeviceToHost, sl.stream));
+    if (status) HIP_TRY(hipMemcpyAsync(status + off, sl.d_status, m, hipMemcpyDeviceToHost, sl.stream));
+    unsigned long long key = kNoBad;
+    HIP_TRY(hipMemcpyAsync(&key, sl.d_key, sizeof key, hipMemcpyDeviceToHost, sl.stream));
+    HIP_TRY(hipStreamSynchronize(sl.stream));
+    if (key != kNoBad && best == kNoBad) best = ((uint64_t)(key >> 8) + off) << 8 | (key & 0xff);
+    return 0;
+  };
+  for (size_t j = 0; j < nchunks; j++) {
+    Slot& sl = c.slot[j & 1];
+    const size_t off = j * chunk, m = std::min(chunk, n - off);
+    HIP_TRY(hipMemcpyAsync(sl.d_in, in + off * rin, m * rin, hipMemcpyHostToDevice, sl.stream));
+    HIP_TRY(hipMemsetAsync(sl.d_key, 0xff, sizeof(unsigned long long), sl.stream));
+    HIP_TRY(launch_codec(op, sl.d_in, sl.d_out, m, flags, sl.d_key, status ? sl.d_status : nullptr, sl.stream));
+    if (j > 0 && drain(j - 1)) return KZGPOT_E_DEVICE;  // chunks finish in order: best stays the first
+  }
+  if (drain(nchunks - 1)) return KZGPOT_E_DEVICE;
   return decode_key(best, first_bad);
 }
 

@@ -86,17 +86,20 @@ def test_no_subgroup_check_mode(gpu, oracle_lib):
 
 
 def test_chunked_host_path_first_bad(gpu, oracle_lib):
-    """> 2^22 points exercise the host API's chunk loop; a bad point in the second chunk must be
-    reported with its global index."""
+    """> 2^22 points run the host API's two-stream chunk pipeline (2^21-point chunks, three of
+    them, so a slot is reused); bad points in the second and third chunks: the smallest global
+    index is reported, every status lands at its global index."""
     base, ark = _random_stream(oracle_lib, 4096, seed=3)
     n = (1 << 22) + 4096
     reps = n // 4096
     data = bytearray(base * reps)
+    first = (1 << 21) + 5
     bad_at = (1 << 22) + 17
     data[bad_at * 48] &= 0x7F
+    data[first * 48] &= 0x7F
     r = gpu.g1_decompress(bytes(data), want_status=True)
-    assert r.ret == -1 and r.first_bad == bad_at
-    assert r.status[bad_at] == 1 and r.status.count(0) == n - 1
+    assert r.ret == -1 and r.first_bad == first
+    assert r.status[bad_at] == 1 and r.status[first] == 1 and r.status.count(0) == n - 2
     assert r.out[:4096 * 96] == ark and r.out[bad_at * 96:(bad_at + 1) * 96] == bytes(96)
 
 
