@@ -164,6 +164,22 @@ int kzgpot_load_fastkzg_setup_buffer(const uint8_t* file, size_t len, uint32_t n
                                      uint8_t* powers_of_gamma_g, uint8_t* h_beta_h, uint8_t* powers_of_h,
                                      int* bad_section, int64_t* bad_index);
 
+/* load_phase1(exp) (src/lib.rs:82-121, Phase1Parameters src/lib.rs:30-39), next-row §8f 3: a
+ * phase1radix2m{exp} file = alpha, beta_g1 (G1), beta_g2 (G2), then coeffs_g1, coeffs_g2,
+ * alpha_coeffs_g1, beta_coeffs_g1 (2^exp points each), every point read by read_g1 / read_g2
+ * (src/lib.rs:41-80: pairing uncompressed, byte reorder, ark deserialize_uncompressed with the
+ * subgroup check) into the in-memory GroupAffine layout (104 / 200 B per point). The reference
+ * hardcodes the path "../phase1radix2m{exp}" (src/lib.rs:84); here it is an argument. Trailing
+ * bytes are ignored; a short file is KZGPOT_E_SIZE. *bad_section: 0 alpha, 1 beta_g1, 2 beta_g2,
+ * 3 coeffs_g1, 4 coeffs_g2, 5 alpha_coeffs_g1, 6 beta_coeffs_g1. */
+uint64_t kzgpot_phase1_size(uint32_t exp);
+int kzgpot_load_phase1(const char* path, uint32_t exp, uint8_t* alpha, uint8_t* beta_g1, uint8_t* beta_g2,
+                       uint8_t* coeffs_g1, uint8_t* coeffs_g2, uint8_t* alpha_coeffs_g1, uint8_t* beta_coeffs_g1,
+                       int* bad_section, int64_t* bad_index);
+int kzgpot_load_phase1_buffer(const uint8_t* file, size_t len, uint32_t exp, uint8_t* alpha, uint8_t* beta_g1,
+                              uint8_t* beta_g2, uint8_t* coeffs_g1, uint8_t* coeffs_g2, uint8_t* alpha_coeffs_g1,
+                              uint8_t* beta_coeffs_g1, int* bad_section, int64_t* bad_index);
+
 /* ---------------------------------------------------------------- BN254 (config 5, next-row §8f 4) */
 /* No reference counterpart: the same path instantiated for ark-bn254 0.2 G1 (cofactor 1).
  * ark compressed (32 B: x LE, SWFlags bit7 PositiveY / bit6 Infinity in byte 31) → ark

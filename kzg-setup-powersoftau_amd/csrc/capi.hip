@@ -519,6 +519,36 @@ int kzgpot_load_kzg_setup(const char* path, uint32_t n_log2, uint8_t* powers_of_
   return kzgpot_load_kzg_setup_buffer(buf.data(), buf.size(), n_log2, powers_of_g, powers_of_gamma_g, vk,
                                       bad_section, bad_index);
 }
+uint64_t kzgpot_phase1_size(uint32_t exp) {
+  if (exp > 30) return 0;
+  const uint64_t m = 1ull << exp;
+  return 2 * 96 + 192 + m * (3 * 96 + 192);
+}
+int kzgpot_load_phase1_buffer(const uint8_t* file, size_t len, uint32_t exp, uint8_t* alpha, uint8_t* beta_g1,
+                              uint8_t* beta_g2, uint8_t* coeffs_g1, uint8_t* coeffs_g2, uint8_t* alpha_coeffs_g1,
+                              uint8_t* beta_coeffs_g1, int* bad_section, int64_t* bad_index) {
+  if (exp > 30) return KZGPOT_E_INVALID_ARG;
+  const uint64_t m = 1ull << exp;
+  const LoadSection secs[] = {
+      {CodecOp::G1Phase1, 1, alpha, 0},            // src/lib.rs:92
+      {CodecOp::G1Phase1, 1, beta_g1, 1},          // src/lib.rs:93
+      {CodecOp::G2Phase1, 1, beta_g2, 2},          // src/lib.rs:94
+      {CodecOp::G1Phase1, m, coeffs_g1, 3},        // src/lib.rs:95-98
+      {CodecOp::G2Phase1, m, coeffs_g2, 4},        // src/lib.rs:99-102
+      {CodecOp::G1Phase1, m, alpha_coeffs_g1, 5},  // src/lib.rs:103-106
+      {CodecOp::G1Phase1, m, beta_coeffs_g1, 6},   // src/lib.rs:107-110
+  };
+  return load_sections(file, len, secs, 7, bad_section, bad_index);
+}
+int kzgpot_load_phase1(const char* path, uint32_t exp, uint8_t* alpha, uint8_t* beta_g1, uint8_t* beta_g2,
+                       uint8_t* coeffs_g1, uint8_t* coeffs_g2, uint8_t* alpha_coeffs_g1, uint8_t* beta_coeffs_g1,
+                       int* bad_section, int64_t* bad_index) {
+  std::vector<uint8_t> buf;
+  const int r = read_file(path, buf);
+  if (r) return r;
+  return kzgpot_load_phase1_buffer(buf.data(), buf.size(), exp, alpha, beta_g1, beta_g2, coeffs_g1, coeffs_g2,
+                                   alpha_coeffs_g1, beta_coeffs_g1, bad_section, bad_index);
+}
 int kzgpot_load_fastkzg_setup_buffer(const uint8_t* file, size_t len, uint32_t n_log2, uint8_t* powers_of_g,
                                      uint8_t* powers_of_gamma_g, uint8_t* h_beta_h, uint8_t* powers_of_h,
                                      int* bad_section, int64_t* bad_index) {

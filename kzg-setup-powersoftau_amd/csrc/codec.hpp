@@ -9,7 +9,12 @@ namespace kzgpot {
 
 constexpr int kBlock = 256;  // 4 waves; one point per lane
 
-enum class CodecOp { G1Decompress, G2Decompress, G1Transcode, G2Transcode, G1Load, G2Load, Bn254G1Decompress };
+// G1Phase1 / G2Phase1: read_g1 / read_g2 straight into the in-memory GroupAffine (load_phase1) —
+// the transcode kernel in place on the input staging buffer, then the loader kernel. Host-buffer
+// API only (run_host owns the staging it overwrites).
+enum class CodecOp {
+  G1Decompress, G2Decompress, G1Transcode, G2Transcode, G1Load, G2Load, Bn254G1Decompress, G1Phase1, G2Phase1
+};
 
 // record sizes on the wire
 constexpr uint64_t in_record(CodecOp op) {
@@ -21,6 +26,8 @@ constexpr uint64_t in_record(CodecOp op) {
     case CodecOp::G1Load: return 96;
     case CodecOp::G2Load: return 192;
     case CodecOp::Bn254G1Decompress: return 32;
+    case CodecOp::G1Phase1: return 96;
+    case CodecOp::G2Phase1: return 192;
   }
   return 0;
 }
@@ -33,6 +40,8 @@ constexpr uint64_t out_record(CodecOp op) {
     case CodecOp::G1Load: return KZGPOT_G1_ARK_MONT_BYTES;
     case CodecOp::G2Load: return KZGPOT_G2_ARK_MONT_BYTES;
     case CodecOp::Bn254G1Decompress: return 64;
+    case CodecOp::G1Phase1: return KZGPOT_G1_ARK_MONT_BYTES;
+    case CodecOp::G2Phase1: return KZGPOT_G2_ARK_MONT_BYTES;
   }
   return 0;
 }

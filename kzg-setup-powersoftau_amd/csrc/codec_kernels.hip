@@ -230,9 +230,12 @@ __global__ void __launch_bounds__(kBlock) k_g2_decompress(const uint4* __restric
 //   Src::ArkInPlace : the record is phase 1's output (ark LE, x ‖ y)           — decompress path
 //   Src::PairingBE  : pairing-uncompressed input; read_g1 (src/lib.rs:41-54) / read_g2
 //                     (src/lib.rs:56-80) byte order is applied on load        — transcode path
+//   Src::PairingBEInPlace : the same, reading and rewriting the records of `out` (load_phase1's
+//                     first stage; no restrict-qualified pointer aliases another)
 // The reference checks no curve equation: points on the curve take the endomorphism test, the
 // rest the exact ark double-and-add by r (divergent, but only for inputs that are not points).
-enum class Src { ArkInPlace, PairingBE };
+enum class Src { ArkInPlace, PairingBE, PairingBEInPlace };
+constexpr bool src_in_place(Src s) { return s != Src::PairingBE; }
 
 template <Src S>
 struct G1Rec {
@@ -254,7 +257,7 @@ __global__ void __launch_bounds__(kBlock) k_g1_check(const uint4* __restrict__ i
                                                      uint8_t* __restrict__ status) {
   const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
-  const uint4* rec = (S == Src::ArkInPlace ? (const uint4*)out : in) + i * 6;
+  const uint4* rec = (src_in_place(S) ? (const uint4*)out : in) + i * 6;
   uint4* dst = out + i * 6;
   int st = 0;
   bool finf;
@@ -301,7 +304,7 @@ __global__ void __launch_bounds__(kBlock) k_g1_check(const uint4* __restrict__ i
     // Phase 1 emits only points with y^2 = x^3 + 4 (it rejects non-residues), so an in-place
     // record is on the curve; a transcode input may not be (the reference never checks).
     bool on_curve = true;
-    if (S == Src::PairingBE) {
+    if (S != Src::ArkInPlace) {
       fp xm, ym, l, r;
       load(xm, ym);
       fp_sqr(l, ym);
@@ -341,7 +344,7 @@ __global__ void __launch_bounds__(kBlock) k_g1_check(const uint4* __restrict__ i
   }
   if (st) {
     store_zero(dst, 6);
-  } else if (S == Src::PairingBE) {
+  } else if (S != Src::ArkInPlace) {
     words x, y;
     G1Rec<S>::load_xy(x, y, opaque(rec));
     y[11] &= 0x3fffffffu;
@@ -377,7 +380,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 
                                                      uint8_t* __restrict__ status) {
   const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
-  const uint4* rec = (S == Src::ArkInPlace ? (const uint4*)out : in) + i * 12;
+  const uint4* rec = (src_in_place(S) ? (const uint4*)out : in) + i * 12;
   uint4* dst = out + i * 12;
   int st = 0;
   bool finf;
@@ -449,7 +452,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 
   }
   if (st) {
     store_zero(dst, 12);
-  } else if (S == Src::PairingBE) {
+  } else if (S != Src::ArkInPlace) {
     words x0, x1, y0, y1;
     G2Rec<S>::load_xy(x0, x1, y0, y1, opaque(rec));
     y1[11] &= 0x3fffffffu;
@@ -493,6 +496,14 @@ hipError_t launch_codec(CodecOp op, const void* d_in, void* d_out, uint64_t n, u
       hipLaunchKernelGGL(k_g2_check<Src::PairingBE>, grid, block, 0, stream, in, out, n, flags, d_first_bad,
                          d_status);
       break;
+    case CodecOp::G1Phase1:  // read_g1 in place on the (caller-owned staging) input, then GroupAffine
+      hipLaunchKernelGGL(k_g1_check<Src::PairingBEInPlace>, grid, block, 0, stream, nullptr, (uint4*)d_in, n, flags,
+                         d_first_bad, d_status);
+      return launch_load(false, d_in, d_out, n, d_first_bad, nullptr, stream);
+    case CodecOp::G2Phase1:
+      hipLaunchKernelGGL(k_g2_check<Src::PairingBEInPlace>, grid, block, 0, stream, nullptr, (uint4*)d_in, n, flags,
+                         d_first_bad, d_status);
+      return launch_load(true, d_in, d_out, n, d_first_bad, nullptr, stream);
     case CodecOp::G1Load:
     case CodecOp::G2Load:
       return launch_load(op == CodecOp::G2Load, d_in, d_out, n, d_first_bad, d_status, stream);

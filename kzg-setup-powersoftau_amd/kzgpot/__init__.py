@@ -6,6 +6,7 @@ C ABI in `include/kzgpot.h`:
   read_g1 / read_g2            src/lib.rs:41-80     (batched: whole record streams per call)
   load_kzg_setup               src/lib.rs:174-195
   load_fastkzg_setup           src/lib.rs:197-228
+  load_phase1                  src/lib.rs:82-121
   download_kzg_setup /
   download_fastkzg_setup       src/lib.rs:166-172   (no network in this build: local file + digest)
   preprocess_kgz /
@@ -42,6 +43,7 @@ ST_OK, ST_COMPRESSION_MODE, ST_UNEXPECTED_INFO, ST_NOT_IN_FIELD = 0, 1, 2, 3
 ST_NOT_ON_CURVE, ST_NOT_IN_SUBGROUP, ST_UNEXPECTED_FLAGS, ST_INFINITY = 4, 5, 6, 7
 SECTIONS = ("tau_g1", "tau_g2", "alpha_g1", "beta_g1", "beta_g2")
 LOAD_SECTIONS = ("powers_of_g", "powers_of_gamma_g", "vk / h, beta_h", "powers_of_h")
+PHASE1_SECTIONS = ("alpha", "beta_g1", "beta_g2", "coeffs_g1", "coeffs_g2", "alpha_coeffs_g1", "beta_coeffs_g1")
 
 
 class KzgPotError(RuntimeError):
@@ -363,3 +365,42 @@ def download_kzg_setup(check_digest: bool, path: str = KZG_SETUP_FILE) -> None:
 
 def download_fastkzg_setup(check_digest: bool, path: str = KZG_SETUP_FILE) -> None:
     _download_setup(FASTKZG_SETUP_FILE_DIGEST, check_digest, path)
+
+
+@dataclass
+class Phase1Parameters:
+    """src/lib.rs:30-39 `Phase1Parameters`: rows / fields are in-memory GroupAffine records
+    (G1 104 B, G2 200 B; include/kzgpot.h)."""
+    alpha: bytes
+    beta_g1: bytes
+    beta_g2: bytes
+    coeffs_g1: object        # (m, 104) uint8
+    coeffs_g2: object        # (m, 200) uint8
+    alpha_coeffs_g1: object  # (m, 104) uint8
+    beta_coeffs_g1: object   # (m, 104) uint8
+
+
+def phase1_size(exp: int) -> int:
+    return int(_lib.load().kzgpot_phase1_size(exp))
+
+
+def load_phase1_buffer(data, exp: int) -> Phase1Parameters:
+    m = 1 << exp
+    ptr, nbytes, keep = _buf(data)
+    g1, g2 = G1_ARK_MONT_BYTES, G2_ARK_MONT_BYTES
+    bufs = [ctypes.create_string_buffer(k) for k in (g1, g1, g2, m * g1, m * g2, m * g1, m * g1)]
+    sec, idx = ctypes.c_int(-1), ctypes.c_int64(-1)
+    r = _lib.load().kzgpot_load_phase1_buffer(ptr, nbytes, exp, *bufs, ctypes.byref(sec), ctypes.byref(idx))
+    del keep
+    if r:
+        raise KzgPotError(r, idx.value, sec.value, PHASE1_SECTIONS)
+    return Phase1Parameters(bufs[0].raw, bufs[1].raw, bufs[2].raw, _records(bufs[3].raw, g1),
+                            _records(bufs[4].raw, g2), _records(bufs[5].raw, g1), _records(bufs[6].raw, g1))
+
+
+def load_phase1(exp: int, path: str | None = None) -> Phase1Parameters:
+    """src/lib.rs:82-121 `load_phase1(exp)`: every point through read_g1 / read_g2 (subgroup
+    check included) on the GPU. The reference opens "../phase1radix2m{exp}" (lib.rs:84): that is
+    the default path here too."""
+    with open(path or f"../phase1radix2m{exp}", "rb") as f:
+        return load_phase1_buffer(f.read(), exp)

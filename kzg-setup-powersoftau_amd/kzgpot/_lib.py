@@ -48,6 +48,9 @@ SIGNATURES = {
     "kzgpot_load_kzg_setup_buffer": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, intp, i64p]),
     "kzgpot_load_fastkzg_setup": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, intp, i64p]),
     "kzgpot_load_fastkzg_setup_buffer": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, intp, i64p]),
+    "kzgpot_phase1_size": (ctypes.c_uint64, [ctypes.c_uint32]),
+    "kzgpot_load_phase1": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_uint32] + [ctypes.c_void_p] * 7 + [intp, i64p]),
+    "kzgpot_load_phase1_buffer": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32] + [ctypes.c_void_p] * 7 + [intp, i64p]),
     "kzgpot_preprocess_ex": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_uint32, ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, intp, i64p]),
     "kzgpot_preprocess_buffer_ex": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32, ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, intp, i64p]),
     "kzgpot_blake2b": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),

@@ -546,6 +546,43 @@ def load_fastkzg_setup(data: bytes, n: int):
     return OK, tuple(outs)
 
 
+def g1_read_to_mont(pairing96: bytes):
+    """read_g1 (src/lib.rs:41-54) → the in-memory GroupAffine it returns (104 B)."""
+    st, apt = read_g1_bytes(pairing96)
+    if st:
+        return st, None
+    x, y, inf = apt
+    return OK, _ark_mont_bytes(x) + _ark_mont_bytes(y) + bytes([1 if inf else 0]) + bytes(7)
+
+
+def g2_read_to_mont(pairing192: bytes):
+    """read_g2 (src/lib.rs:56-80) → in-memory GroupAffine<g2> (200 B)."""
+    st, apt = read_g2_bytes(pairing192)
+    if st:
+        return st, None
+    (x0, x1), (y0, y1), inf = apt
+    return OK, b"".join(_ark_mont_bytes(v) for v in (x0, x1, y0, y1)) + bytes([1 if inf else 0]) + bytes(7)
+
+
+def load_phase1(data: bytes, exp: int):
+    """src/lib.rs:82-121: alpha, beta_g1, beta_g2, then coeffs_g1, coeffs_g2, alpha_coeffs_g1,
+    beta_coeffs_g1 (2^exp each), all through read_g1 / read_g2. → (status, section, index, [7 outs])."""
+    m = 1 << exp
+    plan = [(False, 1), (False, 1), (True, 1), (False, m), (True, m), (False, m), (False, m)]
+    off, outs = 0, []
+    for sec, (g2, count) in enumerate(plan):
+        rec = G2_UNCOMPRESSED if g2 else G1_UNCOMPRESSED
+        if off + count * rec > len(data):
+            raise ValueError("phase1 file too short")
+        fn = g2_read_to_mont if g2 else g1_read_to_mont
+        out, sts, bad = batch(fn, data[off:off + count * rec], rec, G2_ARK_MONT if g2 else G1_ARK_MONT)
+        if bad >= 0:
+            return sts[bad], sec, bad, outs
+        outs.append(out)
+        off += count * rec
+    return OK, -1, -1, outs
+
+
 # ----------------------------------------------------------------------------------------------
 # BN254 G1 (config 5, SURVEY §8f 4 — no reference counterpart): ark-bn254 0.2 compressed G1
 # → ark-ec 0.2 GroupAffine::deserialize → serialize_uncompressed. Same ark rules as the BLS12-381
@@ -772,6 +809,20 @@ def make_response_transcript(n: int, seed: int) -> bytes:
     out += rng.randbytes(PUBLIC_KEY_SIZE)
     assert len(out) == powersoftau_contribution_size(n)
     return bytes(out)
+
+
+def make_phase1_file(exp: int, seed: int) -> bytes:
+    """A phase1radix2m{exp}-layout file (src/lib.rs:82-121): alpha, beta_g1, beta_g2, then
+    coeffs_g1, coeffs_g2, alpha_coeffs_g1, beta_coeffs_g1 (2^exp each), pairing-uncompressed.
+    Synthetic: [a]G1, [b]G1, [b]G2, [c_i]G1, [c_i]G2, [a c_i]G1, [b c_i]G1 for random a, b, c_i."""
+    rng = random.Random(seed)
+    a, b = rng.randrange(1, R_ORDER), rng.randrange(1, R_ORDER)
+    cs = [rng.randrange(1, R_ORDER) for _ in range(1 << exp)]
+    e1 = lambda k: pairing_g1_uncompressed(g1_mul(G1_GEN, k % R_ORDER))  # noqa: E731
+    e2 = lambda k: pairing_g2_uncompressed(g2_mul(G2_GEN, k % R_ORDER))  # noqa: E731
+    parts = [e1(a), e1(b), e2(b)] + [e1(c) for c in cs] + [e2(c) for c in cs] + [e1(a * c) for c in cs] + \
+        [e1(b * c) for c in cs]
+    return b"".join(parts)
 
 
 def _sections(n: int):

@@ -280,3 +280,31 @@ def test_bn254_synth_round_trip(gpu):
         st, want = O.bn254_g1_decompress_point(c[32 * i:32 * i + 32])
         assert st == 0 and want == o[64 * i:64 * i + 64]
 
+
+
+@pytest.mark.gpu
+def test_load_phase1_matches_oracle(gpu):
+    """load_phase1 (src/lib.rs:82-121) on a synthetic phase1radix2m3 file: all seven sections
+    equal the oracle's in-memory GroupAffine records; a non-subgroup point planted in coeffs_g2
+    and one in beta_coeffs_g1 are reported at the first (section 4) with its index."""
+    import kzgpot_oracle as O
+
+    data = bytearray(O.make_phase1_file(3, seed=11))
+    st, _, _, want = O.load_phase1(bytes(data), 3)
+    assert st == O.OK
+    got = gpu.load_phase1_buffer(bytes(data), 3)
+    fields = [got.alpha, got.beta_g1, got.beta_g2, got.coeffs_g1, got.coeffs_g2, got.alpha_coeffs_g1,
+              got.beta_coeffs_g1]
+    for f, w in zip(fields, want):
+        assert bytes(f if isinstance(f, bytes) else f.tobytes()) == w
+    bad2 = next(v for v in golden("g2_transcode") if v["status"] == 5)
+    bad1 = next(v for v in golden("g1_transcode") if v["status"] == 5)
+    off_c2 = 2 * 96 + 192 + 8 * 96
+    data[off_c2 + 5 * 192: off_c2 + 6 * 192] = bytes.fromhex(bad2["in"])
+    off_b1 = off_c2 + 8 * 192 + 8 * 96
+    data[off_b1 + 2 * 96: off_b1 + 3 * 96] = bytes.fromhex(bad1["in"])
+    st, sec, idx, _ = O.load_phase1(bytes(data), 3)
+    assert (st, sec, idx) == (5, 4, 5)
+    with pytest.raises(gpu.KzgPotError) as e:
+        gpu.load_phase1_buffer(bytes(data), 3)
+    assert (e.value.code, e.value.section, e.value.first_bad) == (-5, 4, 5)

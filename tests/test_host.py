@@ -122,3 +122,12 @@ def test_cli_reference_failure_paths(mode, tmp_path):
     assert r.returncode == 101
     assert "The size of `powersoftau` should be 296176, but it's 1000, so something isn't right." in r.stderr
     assert not (tmp_path / "kzg_setup").exists()
+
+
+def test_load_phase1_short_file_is_size_error(kzgpot_mod):
+    """A short phase1 file is KZGPOT_E_SIZE (the reference's read_exact hits EOF and panics),
+    decided before any GPU work."""
+    assert kzgpot_mod.phase1_size(3) == 2 * 96 + 192 + 8 * (3 * 96 + 192)
+    with pytest.raises(kzgpot_mod.KzgPotError) as e:
+        kzgpot_mod.load_phase1_buffer(b"\0" * 100, 3)
+    assert e.value.code == -103

@@ -191,3 +191,24 @@ def test_bn254_spec_and_golden():
             y = int.from_bytes(out[32:], "little")
             assert O.bn_on_curve((x, y))
             assert O.bn254_g1_compress((x, y)) == bytes.fromhex(v["in"])  # round trip
+
+
+def test_phase1_oracle_two_paths():
+    """load_phase1 restatement (read_g1/read_g2 → GroupAffine) equals read → serialize →
+    deserialize_unchecked for every point of a synthetic phase1radix2m3 file; layout size."""
+    import kzgpot_oracle as O
+
+    data = O.make_phase1_file(3, seed=11)
+    assert len(data) == 2 * 96 + 192 + 8 * (3 * 96 + 192)
+    st, sec, idx, outs = O.load_phase1(data, 3)
+    assert st == O.OK and len(outs) == 7
+    off = 0
+    for k, (g2, cnt) in enumerate([(False, 1), (False, 1), (True, 1), (False, 8), (True, 8), (False, 8), (False, 8)]):
+        rec = 192 if g2 else 96
+        for i in range(cnt):
+            raw = data[off + i * rec: off + (i + 1) * rec]
+            s1, ark = (O.g2_transcode_point if g2 else O.g1_transcode_point)(raw)
+            s2, mont = (O.g2_deserialize_unchecked_point if g2 else O.g1_deserialize_unchecked_point)(ark)
+            width = 200 if g2 else 104
+            assert s1 == s2 == O.OK and outs[k][i * width:(i + 1) * width] == mont
+        off += cnt * rec
