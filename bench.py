@@ -348,6 +348,30 @@ def main():
             "points": nt, "launch_ms": tr_ms, "points_per_s": nt / (tr_ms * 1e-3), "algorithmic_bytes_per_point": 192,
             "verified_bit_exact": bool(D.read_key(keyt) == KD.NO_BAD and torch.equal(outt, ark))}
         del pin, outt
+        # 2^20 G1 + 2^20 G2 (the Fp2 square-root path) on one GPU, bit-exact
+        n3 = 1 << 20
+        c31, x31 = D.synth("g1", args.seed + 4, 0, n3, dev, with_expected=True)
+        c32, x32 = D.synth("g2", args.seed + 5, 0, n3, dev, with_expected=True)
+        o31 = torch.empty(n3 * 96, dtype=torch.uint8, device=dev)
+        o32 = torch.empty(n3 * 192, dtype=torch.uint8, device=dev)
+        k3 = torch.empty(2, dtype=torch.int64, device=dev)
+        D.codec_dev("g1_decompress", c31, o31, k3[0:1])
+        D.codec_dev("g2_decompress", c32, o32, k3[1:2])
+        ce = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        ce[0].record()
+        D.codec_dev("g1_decompress", c31, o31, k3[0:1])
+        ce[1].record()
+        D.codec_dev("g2_decompress", c32, o32, k3[1:2])
+        ce[2].record()
+        torch.cuda.synchronize()
+        g1c, g2c = ce[0].elapsed_time(ce[1]), ce[1].elapsed_time(ce[2])
+        next_rows["config3_g1_g2_2e20"] = {
+            "workload": "config 3: 2^20 G1 + 2^20 G2 compressed -> ark uncompressed, subgroup-checked, 1 GPU",
+            "g1_ms": g1c, "g2_ms": g2c, "points_per_s": 2 * n3 / ((g1c + g2c) * 1e-3),
+            "g2_ns_per_point": g2c * 1e6 / n3,
+            "verified_bit_exact": bool(D.read_key(k3[0:1]) == KD.NO_BAD and D.read_key(k3[1:2]) == KD.NO_BAD
+                                       and torch.equal(o31, x31) and torch.equal(o32, x32))}
+        del c31, x31, c32, x32, o31, o32
         # BN254 G1, ark compressed (32 B) -> uncompressed (64 B)
         if args.bn254_log2 > 0:
             nb = 1 << args.bn254_log2
