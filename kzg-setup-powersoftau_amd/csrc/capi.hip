@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <condition_variable>
 #include <deque>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <thread>
@@ -79,11 +80,14 @@ int decode_key(uint64_t key, int64_t* first_bad) {
 // alternate between two slots/streams: while the GPU decodes chunk k, this thread copies chunk
 // k-1's output out and chunk k+1's input in (pageable copies block the host, not the other
 // stream), so PCIe time hides behind the kernels except for the first input and last output.
+// on_chunk (may be null) is called with (first point, count) of each chunk once its output is
+// in `out`, in order — the end-to-end preprocess streams the output digest from it.
+// keep_out = false: the records are validated but not copied back (out may be null).
 int run_host(int dev, CodecOp op, const uint8_t* in, size_t n, uint8_t* out, uint32_t flags, int64_t* first_bad,
-             uint8_t* status) {
+             uint8_t* status, const std::function<void(size_t, size_t)>* on_chunk = nullptr, bool keep_out = true) {
   if (first_bad) *first_bad = -1;
   if (n == 0) return 0;
-  if (!in || !out) return KZGPOT_E_INVALID_ARG;
+  if (!in || (keep_out && !out)) return KZGPOT_E_INVALID_ARG;
   if (dev < 0 || dev >= device_count() || dev >= 64) return KZGPOT_E_DEVICE;
   DevCtx& c = g_ctx[dev];
   std::lock_guard<std::mutex> lock(c.mu);
@@ -104,12 +108,13 @@ int run_host(int dev, CodecOp op, const uint8_t* in, size_t n, uint8_t* out, uin
   auto drain = [&](size_t j) -> int {
     Slot& sl = c.slot[j & 1];
     const size_t off = j * chunk, m = std::min(chunk, n - off);
-    HIP_TRY(hipMemcpyAsync(out + off * rout, sl.d_out, m * rout, hipMemcpyDeviceToHost, sl.stream));
+    if (keep_out) HIP_TRY(hipMemcpyAsync(out + off * rout, sl.d_out, m * rout, hipMemcpyDeviceToHost, sl.stream));
     if (status) HIP_TRY(hipMemcpyAsync(status + off, sl.d_status, m, hipMemcpyDeviceToHost, sl.stream));
     unsigned long long key = kNoBad;
     HIP_TRY(hipMemcpyAsync(&key, sl.d_key, sizeof key, hipMemcpyDeviceToHost, sl.stream));
     HIP_TRY(hipStreamSynchronize(sl.stream));
     if (key != kNoBad && best == kNoBad) best = ((uint64_t)(key >> 8) + off) << 8 | (key & 0xff);
+    if (on_chunk && best == kNoBad) (*on_chunk)(off, m);
     return 0;
   };
   for (size_t j = 0; j < nchunks; j++) {
@@ -260,7 +265,7 @@ int preprocess_impl(const uint8_t* tr, size_t len, uint8_t* out, int mode, uint3
                     int64_t* bad_index) {
   if (bad_section) *bad_section = -1;
   if (bad_index) *bad_index = -1;
-  if (!tr || !out || n_log2 > 30 || (mode != KZGPOT_MODE_KZG && mode != KZGPOT_MODE_FASTKZG))
+  if (!tr || !out || n_log2 < 1 || n_log2 > 30 || (mode != KZGPOT_MODE_KZG && mode != KZGPOT_MODE_FASTKZG))
     return KZGPOT_E_INVALID_ARG;
   if (expect_in_hex && strlen(expect_in_hex) != 128) return KZGPOT_E_INVALID_ARG;
   if (len != kzgpot_contribution_size(n_log2)) return KZGPOT_E_SIZE;
@@ -282,20 +287,11 @@ int preprocess_impl(const uint8_t* tr, size_t len, uint8_t* out, int mode, uint3
   // read back by read_g1/read_g2 (checked) in each binary: kgz τG1, τG2, ατG1; fastkgz + βτG1
   const bool checked[5] = {true, true, true, mode == KZGPOT_MODE_FASTKZG, false};
   // output layout (A7): τG1 and ατG1 are decoded straight into their place in `out`; fastkzg's
-  // powers_of_h (= τG2) too; the rest goes to scratch
+  // powers_of_h (= τG2) too; sections the file does not hold (kgz τG2 beyond h, beta_h; βτG1;
+  // βG2) are decoded and checked on the GPU but never copied back (dst = null)
   const uint64_t off_gamma = (2 * n - 1) * 96, off_tail = off_gamma + n * 96;
-  std::vector<std::vector<uint8_t>> scratch(5);
-  uint8_t* dst[5];
-  for (int s = 0; s < 5; s++) {
-    const uint64_t rout = g2[s] ? 192 : 96;
-    if (s == 0) dst[s] = out;
-    else if (s == 2) dst[s] = out + off_gamma;
-    else if (s == 1 && mode == KZGPOT_MODE_FASTKZG) dst[s] = out + off_tail + 2 * 192;
-    else {
-      scratch[s].resize(cnt[s] * rout);
-      dst[s] = scratch[s].data();
-    }
-  }
+  uint8_t* dst[5] = {out, nullptr, out + off_gamma, nullptr, nullptr};
+  if (mode == KZGPOT_MODE_FASTKZG) dst[1] = out + off_tail + 2 * 192;
   int ret = 0;
   const uint8_t* p = tr + 64;
   for (int s = 0; s < 5 && !ret; s++) {
@@ -307,10 +303,17 @@ int preprocess_impl(const uint8_t* tr, size_t len, uint8_t* out, int mode, uint3
     std::vector<int64_t> fb(n_gpus, -1);
     std::vector<std::thread> th;
     const uint64_t per = (cnt[s] + n_gpus - 1) / n_gpus;
+    // On one GPU the τG1 / ατG1 output (file order) is handed to the digest thread chunk by chunk
+    // as it lands, so hashing the output overlaps the GPU pass instead of following it.
+    const bool stream = out_hash && n_gpus == 1 && (s == 0 || s == 2);
+    const std::function<void(size_t, size_t)> push = [&, s, rout](size_t off, size_t m) {
+      out_hash->push(dst[s] + off * rout, m * rout);
+    };
     for (int g = 0; g < n_gpus; g++) {
       const uint64_t lo = std::min(cnt[s], g * per), hi = std::min(cnt[s], lo + per);
       th.emplace_back([&, g, lo, hi] {
-        rc[g] = run_host(g, op, p + lo * rin, hi - lo, dst[s] + lo * rout, fl, &fb[g], nullptr);
+        rc[g] = run_host(g, op, p + lo * rin, hi - lo, dst[s] ? dst[s] + lo * rout : nullptr, fl, &fb[g], nullptr,
+                         stream ? &push : nullptr, dst[s] != nullptr);
         if (fb[g] >= 0) fb[g] += (int64_t)lo;
       });
     }
@@ -322,12 +325,17 @@ int preprocess_impl(const uint8_t* tr, size_t len, uint8_t* out, int mode, uint3
         if (bad_index) *bad_index = fb[g];
       }
     p += cnt[s] * rin;
-    if (!ret && out_hash && s == 0) out_hash->push(out, off_gamma);
-    if (!ret && out_hash && s == 2) out_hash->push(out + off_gamma, n * 96);
+    if (!ret && out_hash && !stream && s == 0) out_hash->push(out, off_gamma);
+    if (!ret && out_hash && !stream && s == 2) out_hash->push(out + off_gamma, n * 96);
+  }
+  uint8_t h_beta_h[2 * 192];  // kgz: τG2[0..1] for the VerifierKey (the section itself was checked)
+  if (!ret && mode == KZGPOT_MODE_KZG) {
+    int64_t fb2 = -1;
+    ret = run_host(0, CodecOp::G2Decompress, tr + 64 + cnt[0] * 48, 2, h_beta_h, 0, &fb2, nullptr);
   }
   if (!ret) {
     uint8_t* o = out + off_tail;
-    const uint8_t* tau_g2 = mode == KZGPOT_MODE_FASTKZG ? dst[1] : scratch[1].data();
+    const uint8_t* tau_g2 = mode == KZGPOT_MODE_FASTKZG ? dst[1] : h_beta_h;
     if (mode == KZGPOT_MODE_KZG) {  // VerifierKey{g, gamma_g, h, beta_h} (preprocess-kgz.rs:177-194)
       memcpy(o, out, 96);
       memcpy(o + 96, out + off_gamma, 96);
