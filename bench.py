@@ -48,7 +48,7 @@ def parse():
     ap.add_argument("--seed", type=int, default=0x5EED)
     ap.add_argument("--no-gather", action="store_true", help="skip the RCCL all-gather (N > 1)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL, the product path) or gloo (rehearsal)")
-    ap.add_argument("--gather-chunks", type=int, default=4,
+    ap.add_argument("--gather-chunks", type=int, default=8,
                     help="N > 1: G1 chunks per rank; each chunk's all-gather overlaps the next chunk's decode")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
