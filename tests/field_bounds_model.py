@@ -109,6 +109,21 @@ def mul(a: V, b: V, name="mul"):
     return out
 
 
+def mul_sum2(a: V, b: V, c: V, d: V, name="mul_sum2"):
+    """fp_mul_sum2: a b + c d with one Montgomery reduction (three mad chains per column)."""
+    carry = 0
+    for i in range(2 * NL):
+        j0 = 0 if i < NL else i - (NL - 1)
+        j1 = i if i < NL else NL - 1
+        s = sum(a.limbs[j] * b.limbs[i - j] + c.limbs[j] * d.limbs[i - j] for j in range(j0, j1 + 1))
+        s += sum(LM * P_L[i - j] for j in range(j0, j1 + 1))
+        s += carry
+        if s >= 1 << 64:
+            raise BoundError(f"{name}: column {i} may reach {s.bit_length()} bits")
+        carry = s >> LB
+    return normalized(((a.val * b.val + c.val * d.val) * P_OVER_R + 1) * UP, name)
+
+
 def sqr(a: V, name="sqr"):
     """fp_sqr: same column sums as mul(a, a); the doubled operand 2 a_k must fit 32 bits."""
     if max(a.limbs) >= 1 << 31:
@@ -202,16 +217,14 @@ def add_red(a, b, name="add_red"):
 
 
 def f2_mul(a: V2, b: V2, name="f2mul"):
+    """f_mul(fp2): c0 = REDC(a0 b0 + a1 (4p - b1)), c1 = REDC(a0 b1 + a1 b0)."""
     for c in (a.c0, a.c1, b.c0, b.c1):
         check_reduced(c, name)
-    t0 = mul(a.c0, b.c0, name + ".t0")
-    t1 = mul(a.c1, b.c1, name + ".t1")
-    s0 = add_nr(a.c0, a.c1)
-    s1 = add_nr(b.c0, b.c1)
-    s0 = mul(s0, s1, name + ".t2")
-    c0 = sub_red(t0, t1, name + ".c0")
-    t01 = add_red(t0, t1, name + ".t01")
-    return V2(c0, sub_red(s0, t01, name + ".c1"))
+    nb1 = subk(normalized(0), b.c1, "KB_4_28", name + ".nb1")
+    c0 = mul_sum2(a.c0, b.c0, a.c1, nb1, name + ".c0")
+    c1 = mul_sum2(a.c0, b.c1, a.c1, b.c0, name + ".c1")
+    check_reduced(c0, name), check_reduced(c1, name)
+    return V2(c0, c1)
 
 
 def f2_sqr(a: V2, name="f2sqr"):
