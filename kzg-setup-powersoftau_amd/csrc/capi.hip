@@ -6,12 +6,18 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <errno.h>
+#include <fcntl.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <condition_variable>
 #include <deque>
 #include <functional>
 #include <memory>
 #include <mutex>
+#include <new>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -67,6 +73,53 @@ int device_count() {
   return n;
 }
 
+// Restores the caller's current HIP device on scope exit: the library switches devices per
+// shard, and a torch rank on cuda:3 must still be on cuda:3 after any call.
+struct DeviceGuard {
+  int prev = -1;
+  DeviceGuard() {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+// Bytes [0, ready) of a transcript that is still being read from disk are valid; consumers (the
+// GPU chunk loop, the transcript hasher) wait for the range they need.
+class Watermark {
+ public:
+  void advance(size_t to) {
+    std::lock_guard<std::mutex> l(mu_);
+    ready_ = to;
+    cv_.notify_all();
+  }
+  void fail() {
+    std::lock_guard<std::mutex> l(mu_);
+    failed_ = true;
+    cv_.notify_all();
+  }
+  // false if the reader failed before `upto` bytes arrived
+  bool wait(size_t upto) {
+    std::unique_lock<std::mutex> l(mu_);
+    cv_.wait(l, [&] { return failed_ || ready_ >= upto; });
+    return ready_ >= upto;
+  }
+
+ private:
+  std::mutex mu_;
+  std::condition_variable cv_;
+  size_t ready_ = 0;
+  bool failed_ = false;
+};
+
+// Where a run_host input lives while the file is still being read: wait until `end` is readable.
+struct InputWait {
+  Watermark* wm;
+  const uint8_t* base;
+  bool operator()(const uint8_t* end) const { return !wm || wm->wait((size_t)(end - base)); }
+};
+
 int decode_key(uint64_t key, int64_t* first_bad) {
   if (key == kNoBad) {
     if (first_bad) *first_bad = -1;
@@ -83,14 +136,18 @@ int decode_key(uint64_t key, int64_t* first_bad) {
 // on_chunk (may be null) is called with (first point, count) of each chunk once its output is
 // in `out`, in order — the end-to-end preprocess streams the output digest from it.
 // keep_out = false: the records are validated but not copied back (out may be null).
+// in_wait (may be null): called before each chunk's input is copied, for inputs still streaming
+// in from disk.
 int run_host(int dev, CodecOp op, const uint8_t* in, size_t n, uint8_t* out, uint32_t flags, int64_t* first_bad,
-             uint8_t* status, const std::function<void(size_t, size_t)>* on_chunk = nullptr, bool keep_out = true) {
+             uint8_t* status, const std::function<void(size_t, size_t)>* on_chunk = nullptr, bool keep_out = true,
+             const InputWait* in_wait = nullptr) {
   if (first_bad) *first_bad = -1;
   if (n == 0) return 0;
   if (!in || (keep_out && !out)) return KZGPOT_E_INVALID_ARG;
   if (dev < 0 || dev >= device_count() || dev >= 64) return KZGPOT_E_DEVICE;
   DevCtx& c = g_ctx[dev];
   std::lock_guard<std::mutex> lock(c.mu);
+  DeviceGuard guard;
   HIP_TRY(hipSetDevice(dev));
   const uint64_t rin = in_record(op), rout = out_record(op);
   const size_t chunk = std::min<size_t>(n, (size_t)1 << 21);  // 2 x 2^21 x 288 B of staging at most
@@ -120,6 +177,11 @@ int run_host(int dev, CodecOp op, const uint8_t* in, size_t n, uint8_t* out, uin
   for (size_t j = 0; j < nchunks; j++) {
     Slot& sl = c.slot[j & 1];
     const size_t off = j * chunk, m = std::min(chunk, n - off);
+    if (in_wait && !(*in_wait)(in + (off + m) * rin)) {  // the transcript read failed
+      for (int k = 0; k < 2; k++)
+        if (c.slot[k].stream) (void)hipStreamSynchronize(c.slot[k].stream);
+      return KZGPOT_E_IO;
+    }
     HIP_TRY(hipMemcpyAsync(sl.d_in, in + off * rin, m * rin, hipMemcpyHostToDevice, sl.stream));
     HIP_TRY(hipMemsetAsync(sl.d_key, 0xff, sizeof(unsigned long long), sl.stream));
     HIP_TRY(launch_codec(op, sl.d_in, sl.d_out, m, flags, sl.d_key, status ? sl.d_status : nullptr, sl.stream));
@@ -215,27 +277,28 @@ uint64_t kzgpot_output_size(uint32_t n_log2, int mode) {
 
 namespace {
 
-// Hashes byte ranges in submission order on its own thread (BLAKE2b is one sequential stream), so
-// the output digest is computed while the GPU is still decoding later sections.
-class OrderedHasher {
+// Consumes byte ranges in submission order on its own thread: the output digest (BLAKE2b is one
+// sequential stream) and the output file writer, so both run while the GPU is still decoding
+// later sections.
+class OrderedWorker {
  public:
-  OrderedHasher() : th_([this] { run(); }) {}
-  ~OrderedHasher() { finish(nullptr); }
+  explicit OrderedWorker(std::function<bool(const uint8_t*, size_t)> fn) : fn_(std::move(fn)), th_([this] { run(); }) {}
+  ~OrderedWorker() { finish(); }
   void push(const uint8_t* p, size_t n) {
     std::lock_guard<std::mutex> l(mu_);
     q_.emplace_back(p, n);
     cv_.notify_one();
   }
-  // waits for every pushed range; writes the digest if out != nullptr
-  void finish(uint8_t* out) {
+  // waits for every pushed range; false if any range failed
+  bool finish() {
     {
       std::lock_guard<std::mutex> l(mu_);
-      if (done_) return;
+      if (done_) return ok_;
       done_ = true;
       cv_.notify_one();
     }
     th_.join();
-    if (out) h_.finalize(out);
+    return ok_;
   }
 
  private:
@@ -249,20 +312,41 @@ class OrderedHasher {
         item = q_.front();
         q_.pop_front();
       }
-      h_.update(item.first, item.second);
+      if (ok_ && !fn_(item.first, item.second)) ok_ = false;
     }
   }
-  Blake2b h_;
+  std::function<bool(const uint8_t*, size_t)> fn_;
   std::mutex mu_;
   std::condition_variable cv_;
   std::deque<std::pair<const uint8_t*, size_t>> q_;
   bool done_ = false;
+  bool ok_ = true;
   std::thread th_;
 };
 
-int preprocess_impl(const uint8_t* tr, size_t len, uint8_t* out, int mode, uint32_t n_log2, int n_gpus,
-                    const char* expect_in_hex, char* in_hex, char* out_hex, int* bad_section,
-                    int64_t* bad_index) {
+bool pwrite_all(int fd, const uint8_t* p, size_t n, uint64_t off) {
+  while (n) {
+    const ssize_t w = pwrite(fd, p, std::min<size_t>(n, (size_t)1 << 30), (off_t)off);
+    if (w < 0 && errno == EINTR) continue;
+    if (w <= 0) return false;
+    p += w, n -= (size_t)w, off += (uint64_t)w;
+  }
+  return true;
+}
+
+// Where the transcript comes from and where the output goes, besides the two buffers.
+struct PipelineIo {
+  Watermark* in_wm = nullptr;  // non-null: the transcript is still being read from disk
+  int out_fd = -1;             // >= 0: output ranges are written here (file order offsets) as they land
+};
+
+// The two `main`s (preprocess-kgz.rs:162-199, preprocess-fastkgz.rs:180-213) minus the download.
+// n_shards host threads each decode a contiguous shard of every section; shard g runs on device
+// (current + g) % device_count, so n_shards above the device count oversubscribes (the shards of
+// one device then run one after another) — which is how the multi-shard path is tested on one GPU.
+int preprocess_impl(const uint8_t* tr, size_t len, uint8_t* out, int mode, uint32_t n_log2, int n_shards,
+                    const char* expect_in_hex, char* in_hex, char* out_hex, int* bad_section, int64_t* bad_index,
+                    const PipelineIo& io = PipelineIo()) {
   if (bad_section) *bad_section = -1;
   if (bad_index) *bad_index = -1;
   if (!tr || !out || n_log2 < 1 || n_log2 > 30 || (mode != KZGPOT_MODE_KZG && mode != KZGPOT_MODE_FASTKZG))
@@ -271,15 +355,50 @@ int preprocess_impl(const uint8_t* tr, size_t len, uint8_t* out, int mode, uint3
   if (len != kzgpot_contribution_size(n_log2)) return KZGPOT_E_SIZE;
   const int ndev = device_count();
   if (ndev <= 0) return KZGPOT_E_DEVICE;
-  if (n_gpus <= 0 || n_gpus > ndev) n_gpus = ndev;
+  if (n_shards <= 0) n_shards = ndev;
+  n_shards = std::min(n_shards, 64);
+  int dev0 = current_device();
+  if (dev0 < 0 || dev0 >= ndev) dev0 = 0;
   const uint64_t n = 1ull << n_log2;
+  const InputWait in_wait{io.in_wm, tr};
 
-  // transcript digest (download_parameters' check, preprocess-kgz.rs:51-61) beside the GPU pass
+  // transcript digest (download_parameters' check, preprocess-kgz.rs:51-61) beside the GPU pass;
+  // a transcript still streaming from disk is hashed as it arrives
   uint8_t in_digest[64];
+  bool in_ok = true;
   std::thread in_hash;
   const bool want_in = expect_in_hex || in_hex;
-  if (want_in) in_hash = std::thread([&] { blake2b_512(tr, len, in_digest); });
-  std::unique_ptr<OrderedHasher> out_hash(out_hex ? new OrderedHasher() : nullptr);
+  if (want_in)
+    in_hash = std::thread([&] {
+      if (!io.in_wm) return blake2b_512(tr, len, in_digest);
+      Blake2b h;
+      for (size_t off = 0; off < len;) {
+        const size_t m = std::min<size_t>(len - off, (size_t)32 << 20);
+        if (!io.in_wm->wait(off + m)) {
+          in_ok = false;
+          return;
+        }
+        h.update(tr + off, m);
+        off += m;
+      }
+      h.finalize(in_digest);
+    });
+  // output consumers, fed the file's byte ranges in file order
+  Blake2b out_h;
+  std::unique_ptr<OrderedWorker> out_hash, out_write;
+  if (out_hex)
+    out_hash.reset(new OrderedWorker([&](const uint8_t* p, size_t m) {
+      out_h.update(p, m);
+      return true;
+    }));
+  if (io.out_fd >= 0)
+    out_write.reset(new OrderedWorker(
+        [&](const uint8_t* p, size_t m) { return pwrite_all(io.out_fd, p, m, (uint64_t)(p - out)); }));
+  const bool sink = out_hash || out_write;
+  auto push = [&](const uint8_t* p, size_t m) {
+    if (out_hash) out_hash->push(p, m);
+    if (out_write) out_write->push(p, m);
+  };
 
   // powersoftau Accumulator section order (after the 64-B hash)
   const uint64_t cnt[5] = {2 * n - 1, n, n, n, 1};
@@ -298,40 +417,42 @@ int preprocess_impl(const uint8_t* tr, size_t len, uint8_t* out, int mode, uint3
     const CodecOp op = g2[s] ? CodecOp::G2Decompress : CodecOp::G1Decompress;
     const uint64_t rin = in_record(op), rout = out_record(op);
     const uint32_t fl = checked[s] ? 0u : KZGPOT_NO_SUBGROUP_CHECK;
-    // contiguous shards, one host thread per GPU
-    std::vector<int> rc(n_gpus, 0);
-    std::vector<int64_t> fb(n_gpus, -1);
+    // contiguous shards, one host thread each
+    std::vector<int> rc(n_shards, 0);
+    std::vector<int64_t> fb(n_shards, -1);
     std::vector<std::thread> th;
-    const uint64_t per = (cnt[s] + n_gpus - 1) / n_gpus;
-    // On one GPU the τG1 / ατG1 output (file order) is handed to the digest thread chunk by chunk
-    // as it lands, so hashing the output overlaps the GPU pass instead of following it.
-    const bool stream = out_hash && n_gpus == 1 && (s == 0 || s == 2);
-    const std::function<void(size_t, size_t)> push = [&, s, rout](size_t off, size_t m) {
-      out_hash->push(dst[s] + off * rout, m * rout);
+    const uint64_t per = (cnt[s] + n_shards - 1) / n_shards;
+    // With one shard the τG1 / ατG1 output (file order) is handed to the digest and writer threads
+    // chunk by chunk as it lands, so hashing and writing overlap the GPU pass instead of following it.
+    const bool stream = sink && n_shards == 1 && (s == 0 || s == 2);
+    const std::function<void(size_t, size_t)> on_chunk = [&, s, rout](size_t off, size_t m) {
+      push(dst[s] + off * rout, m * rout);
     };
-    for (int g = 0; g < n_gpus; g++) {
+    for (int g = 0; g < n_shards; g++) {
       const uint64_t lo = std::min(cnt[s], g * per), hi = std::min(cnt[s], lo + per);
       th.emplace_back([&, g, lo, hi] {
-        rc[g] = run_host(g, op, p + lo * rin, hi - lo, dst[s] ? dst[s] + lo * rout : nullptr, fl, &fb[g], nullptr,
-                         stream ? &push : nullptr, dst[s] != nullptr);
+        rc[g] = run_host((dev0 + g) % ndev, op, p + lo * rin, hi - lo, dst[s] ? dst[s] + lo * rout : nullptr, fl,
+                         &fb[g], nullptr, stream ? &on_chunk : nullptr, dst[s] != nullptr, &in_wait);
         if (fb[g] >= 0) fb[g] += (int64_t)lo;
       });
     }
     for (auto& t : th) t.join();
-    for (int g = 0; g < n_gpus && !ret; g++)
+    // shards are contiguous and in index order: the first failing shard holds the smallest index
+    for (int g = 0; g < n_shards && !ret; g++)
       if (rc[g]) {
         ret = rc[g];
         if (bad_section) *bad_section = s;
         if (bad_index) *bad_index = fb[g];
       }
     p += cnt[s] * rin;
-    if (!ret && out_hash && !stream && s == 0) out_hash->push(out, off_gamma);
-    if (!ret && out_hash && !stream && s == 2) out_hash->push(out + off_gamma, n * 96);
+    if (!ret && sink && !stream && s == 0) push(out, off_gamma);
+    if (!ret && sink && !stream && s == 2) push(out + off_gamma, n * 96);
   }
   uint8_t h_beta_h[2 * 192];  // kgz: τG2[0..1] for the VerifierKey (the section itself was checked)
   if (!ret && mode == KZGPOT_MODE_KZG) {
     int64_t fb2 = -1;
-    ret = run_host(0, CodecOp::G2Decompress, tr + 64 + cnt[0] * 48, 2, h_beta_h, 0, &fb2, nullptr);
+    ret = run_host(dev0, CodecOp::G2Decompress, tr + 64 + cnt[0] * 48, 2, h_beta_h, 0, &fb2, nullptr, nullptr, true,
+                   &in_wait);
   }
   if (!ret) {
     uint8_t* o = out + off_tail;
@@ -340,23 +461,37 @@ int preprocess_impl(const uint8_t* tr, size_t len, uint8_t* out, int mode, uint3
       memcpy(o, out, 96);
       memcpy(o + 96, out + off_gamma, 96);
       memcpy(o + 192, tau_g2, 384);
-      if (out_hash) out_hash->push(o, 576);
+      if (sink) push(o, 576);
     } else {  // h, beta_h, neg_powers_of_h (empty), powers_of_h (preprocess-fastkgz.rs:200-208)
       memcpy(o, tau_g2, 384);
-      if (out_hash) out_hash->push(o, 384 + n * 192);
+      if (sink) push(o, 384 + n * 192);
     }
   }
+  if (out_write && !out_write->finish() && !ret) ret = KZGPOT_E_IO;
   if (out_hash) {
-    uint8_t d[64];
-    out_hash->finish(d);
-    if (!ret) to_hex(d, out_hex);
+    out_hash->finish();
+    if (!ret) {
+      uint8_t d[64];
+      out_h.finalize(d);
+      to_hex(d, out_hex);
+    }
   }
   if (want_in) {
     in_hash.join();
-    char hex[129];
-    to_hex(in_digest, hex);
-    if (in_hex) memcpy(in_hex, hex, 129);
-    if (!ret && expect_in_hex && strncmp(hex, expect_in_hex, 128) != 0) ret = KZGPOT_E_DIGEST;
+    if (!in_ok) {
+      if (!ret) ret = KZGPOT_E_IO;
+    } else {
+      char hex[129];
+      to_hex(in_digest, hex);
+      if (in_hex) memcpy(in_hex, hex, 129);
+      // The reference checks the digest before it decodes anything (download_parameters runs
+      // first), so a wrong transcript is reported as such even if it also holds a bad point.
+      if (expect_in_hex && strncmp(hex, expect_in_hex, 128) != 0) {
+        ret = KZGPOT_E_DIGEST;
+        if (bad_section) *bad_section = -1;
+        if (bad_index) *bad_index = -1;
+      }
+    }
   }
   return ret;
 }
@@ -382,39 +517,66 @@ int kzgpot_preprocess_buffer(const uint8_t* tr, size_t len, uint8_t* out, int mo
   return preprocess_impl(tr, len, out, mode, n_log2, n_gpus, nullptr, nullptr, nullptr, bad_section, bad_index);
 }
 
+// File to file, as the reference runs (preprocess-kgz.rs:69-126,187-194): a reader thread streams
+// the transcript in 32 MiB pread()s while the GPU decodes what has arrived; a writer thread
+// pwrite()s each output range as it lands. The output goes to a temporary file in the same
+// directory, renamed over `out_path` only on success (the reference's File::create leaves a
+// truncated file behind on a panic).
 int kzgpot_preprocess_ex(const char* transcript_path, const char* out_path, int mode, uint32_t n_log2, int n_gpus,
                          const char* expect_transcript_digest, char* transcript_digest, char* output_digest,
                          int* bad_section, int64_t* bad_index) {
-  if (!transcript_path || !out_path) return KZGPOT_E_INVALID_ARG;
-  FILE* f = fopen(transcript_path, "rb");
-  if (!f) return KZGPOT_E_IO;
-  fseek(f, 0, SEEK_END);
-  const long len = ftell(f);
-  fseek(f, 0, SEEK_SET);
-  if (len < 0 || (uint64_t)len != kzgpot_contribution_size(n_log2)) {
-    fclose(f);
-    return KZGPOT_E_SIZE;
+  if (bad_section) *bad_section = -1;
+  if (bad_index) *bad_index = -1;
+  if (!transcript_path || !out_path || n_log2 < 1 || n_log2 > 30) return KZGPOT_E_INVALID_ARG;
+  const int fd = open(transcript_path, O_RDONLY | O_CLOEXEC);
+  if (fd < 0) return KZGPOT_E_IO;
+  const off_t flen = lseek(fd, 0, SEEK_END);
+  if (flen < 0 || (uint64_t)flen != kzgpot_contribution_size(n_log2)) {
+    close(fd);
+    return flen < 0 ? KZGPOT_E_IO : KZGPOT_E_SIZE;
   }
-  std::vector<uint8_t> tr((size_t)len);
-  const size_t got = fread(tr.data(), 1, tr.size(), f);
-  fclose(f);
-  if (got != tr.size()) return KZGPOT_E_IO;
-  std::vector<uint8_t> out(kzgpot_output_size(n_log2, mode));
-  const int r = preprocess_impl(tr.data(), tr.size(), out.data(), mode, n_log2, n_gpus, expect_transcript_digest,
-                                transcript_digest, output_digest, bad_section, bad_index);
-  if (r) return r;
-  FILE* o = fopen(out_path, "wb");
-  if (!o) return KZGPOT_E_IO;
-  const size_t put = fwrite(out.data(), 1, out.size(), o);
-  const int cr = fclose(o);
-  return (put == out.size() && cr == 0) ? 0 : KZGPOT_E_IO;
+  const size_t len = (size_t)flen;
+  (void)posix_fadvise(fd, 0, flen, POSIX_FADV_SEQUENTIAL);
+  std::unique_ptr<uint8_t[]> tr(new (std::nothrow) uint8_t[len]);
+  std::unique_ptr<uint8_t[]> out(new (std::nothrow) uint8_t[kzgpot_output_size(n_log2, mode)]);
+  if (!tr || !out) {
+    close(fd);
+    return KZGPOT_E_INVALID_ARG;
+  }
+  std::string tmp = std::string(out_path) + ".kzgpot-tmp-" + std::to_string((long)getpid());
+  const int ofd = open(tmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+  if (ofd < 0) {
+    close(fd);
+    return KZGPOT_E_IO;
+  }
+  Watermark wm;
+  std::thread reader([&] {
+    for (size_t off = 0; off < len;) {
+      const ssize_t r = pread(fd, tr.get() + off, std::min<size_t>(len - off, (size_t)32 << 20), (off_t)off);
+      if (r < 0 && errno == EINTR) continue;
+      if (r <= 0) return wm.fail();
+      off += (size_t)r;
+      wm.advance(off);
+    }
+  });
+  PipelineIo io;
+  io.in_wm = &wm;
+  io.out_fd = ofd;
+  int r = preprocess_impl(tr.get(), len, out.get(), mode, n_log2, n_gpus, expect_transcript_digest,
+                          transcript_digest, output_digest, bad_section, bad_index, io);
+  if (r) wm.fail();  // (the reader finishes its current pread and stops; nothing waits on it)
+  reader.join();
+  close(fd);
+  if (close(ofd) != 0 && !r) r = KZGPOT_E_IO;
+  if (!r && rename(tmp.c_str(), out_path) != 0) r = KZGPOT_E_IO;
+  if (r) unlink(tmp.c_str());
+  return r;
 }
 int kzgpot_preprocess(const char* transcript_path, const char* out_path, int mode, uint32_t n_log2, int n_gpus,
                       int* bad_section, int64_t* bad_index) {
   return kzgpot_preprocess_ex(transcript_path, out_path, mode, n_log2, n_gpus, nullptr, nullptr, nullptr,
                               bad_section, bad_index);
 }
-
 // ------------------------------------------------------------------------------- loader mirror
 int kzgpot_g1_deserialize_unchecked_ex(const uint8_t* in, size_t n, uint8_t* out, int64_t* first_bad,
                                        uint8_t* status) {
