@@ -13,10 +13,12 @@ arkworks buffer on every rank (strong scaling: the transcript is fixed, ranks sp
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
 Prints ONE JSON line (rank 0). `roofline` is for the dominant kernel pair (G1 decompress + G1
-check), timed with HIP events on the launch stream; `cpu_baseline` times the C restatement of the
-reference's CPU path (oracle/kzgpot_ref.c, kind "port" — the Rust reference cannot be built
-here) on a bounded sample of the same points, with the reference's schedule (decompression on
-all cores, the arkworks check on one thread).
+check), timed with HIP events on the launch stream; `valu` prices the same launches against the
+cycle-weighted integer-VALU issue roof (profiles/r02_valu_mix.json); `cpu_baseline` times the C
+restatement of the reference's CPU path (oracle/kzgpot_ref.c, kind "port" — the Rust reference
+cannot be built here) on a bounded sample of the same points, with the reference's schedule
+(decompression on all cores, the arkworks check on one thread). `next_rows.bn254_g1_decompress`
+is config 5 (BN254 2^28 G1), sharded and all-gathered exactly like config 4 at N > 1.
 """
 from __future__ import annotations
 
@@ -25,17 +27,21 @@ import ctypes
 import json
 import os
 import sys
+import tempfile
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "kzg-setup-powersoftau_amd"))
 
 HBM_PEAK_GBS = 8000.0           # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-# integer-VALU issue roof: 256 CUs x 4 SIMDs, one wave64 VALU instruction per 4 cycles per SIMD
-# (16 lanes) at the 2.4 GHz peak engine clock = 614.4 G wave-instructions/s (MI355X_MICROARCH.md)
-VALU_PEAK_WAVE_INSTR = 256 * 4 * 2.4e9 / 4
-ALG_BYTES_G1 = 144              # 48 B read + 96 B written per G1 point
-ALG_BYTES_G2 = 288
+SIMDS, CLOCK_HZ = 256 * 4, 2.4e9  # MI355X: 256 CUs x 4 SIMDs at the 2.4 GHz peak engine clock
+ALG_BYTES = {"g1": 144, "g2": 288, "bn254": 96}  # bytes read + written per point
+# kernel -> its name in profiles/r02_valu_mix.json (demangled; the check kernels' Src 0 = ArkInPlace)
+MIX_NAMES = {"k_g1_decompress": "kzgpot::k_g1_decompress(", "k_g1_check": "kzgpot::k_g1_check<(kzgpot::Src)0>",
+             "k_g2_decompress": "kzgpot::k_g2_decompress(", "k_g2_check": "kzgpot::k_g2_check<(kzgpot::Src)0>",
+             "k_bn254_g1_decompress": "kzgpot::k_bn254_g1_decompress("}
+RECORDS = {"g1": (48, 96, "g1_decompress"), "g2": (96, 192, "g2_decompress"),
+           "bn254": (32, 64, "bn254_g1_decompress")}
 
 
 def parse():
@@ -49,28 +55,37 @@ def parse():
     ap.add_argument("--no-gather", action="store_true", help="skip the RCCL all-gather (N > 1)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL, the product path) or gloo (rehearsal)")
     ap.add_argument("--gather-chunks", type=int, default=8,
-                    help="N > 1: G1 chunks per rank; each chunk's all-gather overlaps the next chunk's decode")
+                    help="N > 1: chunks per rank; each chunk's all-gather overlaps the next chunk's decode")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--oracle-sample-runs", type=int, default=64,
+                    help="runs of 256 output records (+ the last 256) re-decoded by the C oracle")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-log2", type=int, default=15)
-    ap.add_argument("--no-next-rows", action="store_true", help="skip the loader / BN254 (SURVEY 8f) measurements")
+    ap.add_argument("--no-next-rows", action="store_true", help="skip the SURVEY 8f rows and config 5")
     ap.add_argument("--bn254-log2", type=int, default=28, help="config 5 size (0 = skip)")
     ap.add_argument("--e2e-log2", type=int, default=21, help="end-to-end preprocess N (0 = skip)")
     return ap.parse_args()
 
 
+def oracle_lib():
+    path = os.path.join(ROOT, "oracle", "_build", "libkzgpot_oracle.so")
+    return ctypes.CDLL(path) if os.path.exists(path) else None
+
+
+def cpu_cores():
+    return min(os.cpu_count() or 1, 16)  # the GPU box grants 16 CPUs per GPU
+
+
 def cpu_baseline(comp1, comp2, sample_log2):
     """Reference-schedule CPU timing of the oracle restatement on a bounded sample."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    lib_path = os.path.join(ROOT, "oracle", "_build", "libkzgpot_oracle.so")
-    if not os.path.exists(lib_path):
+    lib = oracle_lib()
+    if lib is None:
         return None
-    lib = ctypes.CDLL(lib_path)
     s1 = min(1 << sample_log2, comp1.numel() // 48)
     s2 = max(1, min(s1 >> 11, comp2.numel() // 96))  # keep the workload's G1:G2 ratio (2^27 : 2^16)
     h1 = bytes(comp1[: s1 * 48].cpu().numpy())
     h2 = bytes(comp2[: s2 * 96].cpu().numpy())
-    cores = min(os.cpu_count() or 1, 16)  # the GPU box grants 16 CPUs per GPU
+    cores = cpu_cores()
     o1 = ctypes.create_string_buffer(s1 * 96)
     o2 = ctypes.create_string_buffer(s2 * 192)
     fb = ctypes.c_int64()
@@ -94,11 +109,9 @@ def cpu_baseline(comp1, comp2, sample_log2):
     }
 
 
-def pmc_profile():
-    """The committed rocprofv3 PMC summary (tools/pmc_summary.py -> profiles/pmc_traffic.json)."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+def load_json(name):
     try:
-        return json.load(open(path))
+        return json.load(open(os.path.join(ROOT, "profiles", name)))
     except (OSError, ValueError):
         return None
 
@@ -111,25 +124,204 @@ def pmc_traffic(pmc, n_g1_local):
         return None
 
 
-def valu_roofline(pmc, n_g1_local, g1_ms):
-    """Integer-VALU roof of the G1 codec: PMC SQ_INSTS_VALU per wave (= the instruction stream one
-    lane runs for its point) x waves per launch / the event-timed launch time, against the issue
-    peak. This, not HBM, is the roof that binds."""
+def valu_roofline(pmc, mix, kernels, points, ms):
+    """Integer-VALU roof of a kernel group: PMC SQ_INSTS_VALU per wave (the instruction stream one
+    lane runs for its point) x waves / the event-timed launch time, against the SIMDs' issue rate
+    for THAT instruction mix — each opcode priced at its measured SIMD cycles per wave64
+    instruction (tools/microbench/valu_issue.hip -> profiles/r02_valu_issue_microbench.txt;
+    v_mad_u64_u32 4.4, v_add_u32 2.1, other VOP3 ~4.2), weighted by the kernel's opcode histogram
+    (tools/valu_mix.py -> profiles/r02_valu_mix.json)."""
     try:
-        per_pt = sum(pmc["kernels"][k]["valu_insts_per_wave"] for k in ("k_g1_decompress", "k_g1_check"))
-    except (TypeError, KeyError):
+        insts = [pmc["kernels"][k]["valu_insts_per_wave"] for k in kernels]
+        costs = [next(e["avg_cycles_per_valu"] for name, e in mix["kernels"].items() if MIX_NAMES[k] in name)
+                 for k in kernels]
+    except (TypeError, KeyError, StopIteration):
         return None
-    achieved = per_pt * (n_g1_local / 64) / (g1_ms * 1e-3)
-    return {"valu_instr_per_g1_point": per_pt, "achieved_wave_instr_per_s": achieved,
-            "peak_wave_instr_per_s": VALU_PEAK_WAVE_INSTR, "frac": achieved / VALU_PEAK_WAVE_INSTR,
-            "source": "instruction counts: profiles/pmc_traffic.json (SQ_INSTS_VALU); time: this run"}
+    per_pt = sum(insts)
+    avg_cost = sum(i * c for i, c in zip(insts, costs)) / per_pt
+    peak = SIMDS * CLOCK_HZ / avg_cost
+    achieved = per_pt * (points / 64) / (ms * 1e-3)
+    return {"kernels": kernels, "valu_instr_per_point": per_pt, "avg_simd_cycles_per_instr": avg_cost,
+            "achieved_wave_instr_per_s": achieved, "peak_wave_instr_per_s": peak, "frac": achieved / peak,
+            "source": "instruction counts: profiles/pmc_traffic.json (SQ_INSTS_VALU); per-opcode SIMD cycles: "
+                      "profiles/r02_valu_issue_microbench.txt weighted by profiles/r02_valu_mix.json; "
+                      "peak = 1024 SIMDs x 2.4 GHz / avg cycles; time: this run"}
+
+
+class Sharded:
+    """One point stream of n records decoded across the ranks. N > 1 with the gather: block-cyclic
+    (kzgpot/dist.py) in `chunks` chunks whose in-place all-gathers overlap the next chunk's
+    decoding, into one contiguous arkworks buffer on every rank; otherwise one contiguous shard."""
+
+    def __init__(self, kind, n, seed, chunks, rank, world, gather, dev, verify):
+        import torch
+
+        from kzgpot import device as D
+        from kzgpot import dist as KD
+
+        self.D, self.KD, self.torch = D, KD, torch
+        self.kind, self.n, self.seed, self.rank, self.world, self.gather = kind, n, seed, rank, world, gather
+        self.rin, self.rout, self.op = RECORDS[kind]
+        if gather:
+            b = KD.cyclic_block(n, world, chunks)
+            self.blocks = [(g, b) for g in KD.owned_block_starts(n, rank, world, chunks)]
+        else:
+            lo, hi = KD.shard_bounds(n, rank, world)
+            self.blocks = [(lo, hi - lo)]
+        self.m = sum(c for _, c in self.blocks)
+        parts = [D.synth(kind, seed, g, c, dev, with_expected=verify) for g, c in self.blocks]
+        self.comp = torch.cat([p[0] for p in parts]) if len(parts) > 1 else parts[0][0]
+        self.exps = [p[1] for p in parts]
+        self.out = torch.empty((n if gather else self.m) * self.rout, dtype=torch.uint8, device=dev)
+        self.keys = torch.empty(len(self.blocks), dtype=torch.int64, device=dev)  # one first-bad key per launch
+
+    def dst(self, c):
+        g0, cnt = self.blocks[c]
+        off = g0 if self.gather else sum(x for _, x in self.blocks[:c])
+        return self.out[off * self.rout:(off + cnt) * self.rout]
+
+    def launch(self, c, marks):
+        cnt = self.blocks[c][1]
+        src = self.comp[sum(x for _, x in self.blocks[:c]) * self.rin:][:cnt * self.rin]
+        e = None
+        if marks is not None:
+            e = [self.torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            e[0].record()
+        self.D.codec_dev(self.op, src, self.dst(c), self.keys[c:c + 1])
+        if marks is not None:
+            e[1].record()
+            marks.append((self.kind, e))
+
+    def step(self, marks):
+        """Launch every block; returns the collective handles (wait on them before reading out)."""
+        if self.gather:
+            return self.KD.decode_gather_pipelined(lambda c, g0, dst: self.launch(c, marks), self.out, self.rout,
+                                                   self.n, self.rank, self.world, len(self.blocks))
+        for c in range(len(self.blocks)):
+            self.launch(c, marks)
+        return []
+
+    def bad_key(self):
+        return min(self.KD.key_with_offset(self.D.read_key(self.keys[c:c + 1]), self.blocks[c][0])
+                   for c in range(len(self.blocks)))
+
+    def verify(self):
+        """Own blocks bit-exact against the generator's expected ark bytes; blocks decoded by the
+        other ranks by two 64-bit checksums against their owners'."""
+        torch, dist = self.torch, self.KD.dist
+        ok = self.bad_key() == self.KD.NO_BAD
+        for c, e in enumerate(self.exps):
+            ok = ok and torch.equal(self.dst(c), e)
+        if self.gather and self.world > 1:
+            b = self.blocks[0][1]
+            nb = self.out.numel() // (b * self.rout)
+            mine = torch.zeros(nb, 2, dtype=torch.int64, device=self.out.device)
+            w = torch.arange(1, b * self.rout // 8 + 1, dtype=torch.int64, device=self.out.device)
+            for (g0, cnt), e in zip(self.blocks, self.exps):
+                v = e.view(torch.int64)
+                mine[g0 // cnt] = torch.stack([v.sum(), (v * w).sum()])
+            dist.all_reduce(mine)  # each block has exactly one owner
+            got = self.out.view(torch.int64).view(nb, -1)
+            ok = ok and torch.equal(torch.stack([got.sum(1), (got * w).sum(1)], 1), mine)
+        self.exps = None
+        return bool(ok)
+
+
+def all_ok(ok, world, dev):
+    import torch
+    import torch.distributed as dist
+
+    if world > 1:
+        t = torch.tensor([1 if ok else 0], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        ok = bool(t.item())
+    return ok
+
+
+def timed(streams, steps, warmup, world, dev, verify):
+    """W untimed warm-up steps, (verification), then EXACTLY `steps` steps bracketed by a barrier +
+    synchronize; returns (max-over-ranks seconds, per-step event marks, verified)."""
+    import torch
+    import torch.distributed as dist
+
+    def step(marks):
+        works = []
+        for s in streams:
+            works += s.step(marks)
+        for w in works:
+            w.wait()  # the current stream waits for the collectives
+
+    for _ in range(warmup):
+        step(None)
+    torch.cuda.synchronize()
+    verified = None
+    if verify:
+        if warmup == 0:
+            step(None)
+            torch.cuda.synchronize()
+        verified = all_ok(all(s.verify() for s in streams), world, dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev = []
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        marks = []
+        step(marks)
+        ev.append(marks)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed, ev, verified
+
+
+def kernel_ms(ev, kind):
+    """Average per-step event time of one kind's launches (on the launch stream)."""
+    return sum(e[0].elapsed_time(e[1]) for marks in ev for k, e in marks if k == kind) / max(1, len(ev))
+
+
+def oracle_sample_check(stream, runs):
+    """Independent re-decode of the FULL-size output by the C oracle: `runs`
+    runs of 256 records spread evenly over the whole stream plus its last 256 records (past the
+    4 GiB output offset), their compressed inputs regenerated by index; bytes and accept/reject
+    must equal the oracle's (the reference algorithm: pairing sqrt + ark mul_bits(r) check)."""
+    lib = oracle_lib()
+    if lib is None or runs <= 0:
+        return None
+    n, D = stream.n, stream.D
+    starts = sorted(set([k * (n // runs) for k in range(runs)] + [n - 256]))
+    fn = {"g1": lib.oracle_g1_decompress, "g2": lib.oracle_g2_decompress}.get(stream.kind)
+    if fn is None:
+        return None
+    cores, ok, pts = cpu_cores(), True, 0
+    t = time.perf_counter()
+    for s in starts:
+        g = stream.out[s * stream.rout:(s + 256) * stream.rout]  # gathered buffer (or the N = 1 output)
+        comp, _ = D.synth(stream.kind, stream.seed, s, 256, stream.out.device, with_expected=False)
+        data = bytes(comp.cpu().numpy())
+        want = ctypes.create_string_buffer(256 * stream.rout)
+        st = ctypes.create_string_buffer(256)
+        fb = ctypes.c_int64(-1)
+        r = fn(data, ctypes.c_size_t(256), want, 0, ctypes.byref(fb), st, cores, cores)
+        ok = ok and r == 0 and fb.value == -1 and st.raw == bytes(256) and bytes(g.cpu().numpy()) == want.raw
+        pts += 256
+    return {"kind": stream.kind, "points": pts, "runs": len(starts), "last_record_offset_bytes": (n - 1) * stream.rout,
+            "oracle": "oracle/kzgpot_ref.c (reference algorithms: Fq sqrt a^((p-3)/4), ark mul_bits(r) subgroup)",
+            "equal": bool(ok), "seconds": time.perf_counter() - t}
 
 
 def e2e_preprocess(n_log2, seed, dev, kzgpot, D):
     """Build a synthetic response transcript (powersoftau layout, GPU-generated valid points) and
-    time the C ABI entry kzgpot_preprocess_buffer_ex on it in both modes (host buffers in and out,
-    the output buffer pre-faulted; the Python wrapper's extra copies are not the product); check
-    the τG1 / ατG1 sections and both digests against hashlib."""
+    time the C ABI end to end in both modes: kzgpot_preprocess_buffer_ex (host buffers in and
+    out, the output buffer pre-faulted; the Python wrapper's extra copies are not the product)
+    and kzgpot_preprocess_ex (file to file, as the reference runs: the transcript streamed from
+    disk behind the GPU, the output written behind it). Checks the τG1 / ατG1 sections and both
+    digests against hashlib, and the written file against the buffer output."""
     import hashlib
 
     import numpy as np
@@ -152,6 +344,16 @@ def e2e_preprocess(n_log2, seed, dev, kzgpot, D):
     lib = _lib.load()
     out = np.ones(max(kzgpot.output_size(n_log2, m) for m in (kzgpot.MODE_KZG, kzgpot.MODE_FASTKZG)), np.uint8)
     rows = {}
+    tmpdir = tempfile.mkdtemp(prefix="kzgpot_e2e_")
+    src = os.path.join(tmpdir, "powersoftau")
+    tr.tofile(src)
+    # the file's pure read time (page cache, as the driver's box leaves it after writing it)
+    t0 = time.perf_counter()
+    with open(src, "rb", buffering=0) as f:
+        buf = bytearray(tr.size)
+        f.readinto(buf)
+    read_s = time.perf_counter() - t0
+    del buf
     for mode, name in ((kzgpot.MODE_KZG, "preprocess_kgz_e2e"), (kzgpot.MODE_FASTKZG, "preprocess_fastkgz_e2e")):
         size = kzgpot.output_size(n_log2, mode)
         sec, idx = ctypes.c_int(-1), ctypes.c_int64(-1)
@@ -163,13 +365,31 @@ def e2e_preprocess(n_log2, seed, dev, kzgpot, D):
         g1n = (2 * n - 1) * 96
         ok = r == 0 and np.array_equal(out[:g1n], expect["tau_g1"]) and \
             np.array_equal(out[g1n:g1n + n * 96], expect["alpha_g1"])
-        ok = ok and din.value.decode() == tr_digest and dout.value.decode() == hashlib.blake2b(out[:size]).hexdigest()
+        buf_digest = hashlib.blake2b(out[:size]).hexdigest()
+        ok = ok and din.value.decode() == tr_digest and dout.value.decode() == buf_digest
         pts = (2 * n - 1) + 3 * n + 1
         rows[name] = {"workload": f"N = 2^{n_log2} response transcript ({tr.size} B) -> {size} B file, "
                                   "host buffers, 1 GPU, BLAKE2b of input and output (C ABI call timed)",
                       "seconds": dt, "points": pts, "points_per_s": pts / dt, "sections_verified": bool(ok),
                       "transcript_blake2b": din.value.decode()[:16] + "...",
                       "output_blake2b": dout.value.decode()[:16] + "..."}
+        # file to file (the reference's contract, preprocess-kgz.rs:69-126,187-194)
+        dst = os.path.join(tmpdir, "out")
+        t0 = time.perf_counter()
+        r = lib.kzgpot_preprocess_ex(src.encode(), dst.encode(), mode, n_log2, 1, None, din, dout,
+                                     ctypes.byref(sec), ctypes.byref(idx))
+        dtf = time.perf_counter() - t0
+        with open(dst, "rb") as f:
+            file_digest = hashlib.blake2b(f.read()).hexdigest()
+        os.unlink(dst)
+        rows[name + "_file"] = {
+            "workload": f"same, file to file: kzgpot_preprocess_ex({tr.size} B transcript on local disk -> output "
+                        "file), transcript pread() behind the GPU, output pwrite() behind it, both digests",
+            "seconds": dtf, "points_per_s": pts / dtf, "buffer_path_s": dt, "transcript_read_s": read_s,
+            "vs_buffer_plus_read": dtf / (dt + read_s),
+            "file_verified": bool(r == 0 and file_digest == buf_digest == dout.value.decode())}
+    os.unlink(src)
+    os.rmdir(tmpdir)
     return rows
 
 
@@ -200,135 +420,56 @@ def main():
 
     n1, n2 = 1 << args.g1_log2, 1 << args.g2_log2
     gather = world > 1 and not args.no_gather
-    # Which points this rank decodes, as (global start, count) blocks. N > 1 with the gather:
-    # block-cyclic (kzgpot/dist.py) — G1 in `--gather-chunks` chunks whose all-gathers overlap the
-    # next chunk's decoding, G2 (2^16 points) in one. Otherwise one contiguous shard per rank.
-    if gather:
-        ch1 = args.gather_chunks
-        b1, b2 = KD.cyclic_block(n1, world, ch1), KD.cyclic_block(n2, world, 1)
-        blocks1 = [(g, b1) for g in KD.owned_block_starts(n1, rank, world, ch1)]
-        blocks2 = [(g, b2) for g in KD.owned_block_starts(n2, rank, world, 1)]
-    else:
-        lo1, hi1 = KD.shard_bounds(n1, rank, world)
-        lo2, hi2 = KD.shard_bounds(n2, rank, world)
-        blocks1, blocks2 = [(lo1, hi1 - lo1)], [(lo2, hi2 - lo2)]
-    m1, m2 = sum(c for _, c in blocks1), sum(c for _, c in blocks2)
-
-    def synth(kind, seed, blocks):
-        parts = [D.synth(kind, seed, g, c, dev, with_expected=not args.no_verify) for g, c in blocks]
-        comp = torch.cat([p[0] for p in parts]) if len(parts) > 1 else parts[0][0]
-        return comp, [p[1] for p in parts]
-
+    verify = not args.no_verify
     t_gen = time.perf_counter()
-    comp1, exp1 = synth("g1", args.seed, blocks1)
-    comp2, exp2 = synth("g2", args.seed + 1, blocks2)
+    g1 = Sharded("g1", n1, args.seed, args.gather_chunks, rank, world, gather, dev, verify)
+    g2 = Sharded("g2", n2, args.seed + 1, 1, rank, world, gather, dev, verify)  # 2^16 points: one chunk
     torch.cuda.synchronize()
     t_gen = time.perf_counter() - t_gen
-    # outputs: the full contiguous arkworks buffers (gather) or this rank's shard
-    out1 = torch.empty((n1 if gather else m1) * 96, dtype=torch.uint8, device=dev)
-    out2 = torch.empty((n2 if gather else m2) * 192, dtype=torch.uint8, device=dev)
-    keys1 = torch.empty(len(blocks1), dtype=torch.int64, device=dev)  # one first-bad key per launch
-    keys2 = torch.empty(len(blocks2), dtype=torch.int64, device=dev)
 
-    def dst_of(out, blocks, c, rec):
-        """Where block c of this rank lands in `out`."""
-        g0, cnt = blocks[c]
-        off = g0 if gather else sum(x for _, x in blocks[:c])
-        return out[off * rec:(off + cnt) * rec]
+    elapsed, ev, verified = timed([g1, g2], args.steps, args.warmup, world, dev, verify)
+    bad = KD.allreduce_min_key(min(g1.bad_key(), g2.bad_key()), dev) if world > 1 else min(g1.bad_key(), g2.bad_key())
+    sample = None
+    if verify and rank == 0 and (gather or world == 1):
+        sample = oracle_sample_check(g1, args.oracle_sample_runs)
+    g1_ms, g2_ms = kernel_ms(ev, "g1"), kernel_ms(ev, "g2")
 
-    ev = []
+    next_rows = {} if not args.no_next_rows else None
+    # BN254 G1, ark compressed (32 B) -> uncompressed (64 B),
+    # sharded and gathered across the ranks like config 4 (every rank takes part)
+    if next_rows is not None and args.bn254_log2 > 0:
+        del g1.comp
+        nb = 1 << args.bn254_log2
+        t_bn = time.perf_counter()
+        bn = Sharded("bn254", nb, args.seed + 2, args.gather_chunks, rank, world, gather, dev, verify)
+        torch.cuda.synchronize()
+        t_bn = time.perf_counter() - t_bn
+        bn_s, bn_ev, bn_ok = timed([bn], args.steps, 1, world, dev, verify)
+        bn_bad = KD.allreduce_min_key(bn.bad_key(), dev) if world > 1 else bn.bad_key()
+        bn_ms = kernel_ms(bn_ev, "bn254")
+        next_rows["bn254_g1_decompress"] = {
+            "workload": f"config 5: 2^{args.bn254_log2} BN254 G1, ark compressed 32 B -> ark uncompressed 64 B"
+                        + (f", block-cyclic shards over {world} GPUs, RCCL all-gather to one contiguous buffer "
+                           f"pipelined in {args.gather_chunks} chunks" if gather else ""),
+            "kernel": "k_bn254_g1_decompress", "points": nb, "n_gpus": world, "steps": args.steps,
+            "ms_per_step": bn_s * 1e3 / args.steps, "points_per_s": nb * args.steps / bn_s,
+            "launch_ms_per_rank": bn_ms, "algorithmic_bytes_per_point": ALG_BYTES["bn254"],
+            "achieved_GBs": ALG_BYTES["bn254"] * bn.m / (bn_ms * 1e-3) / 1e9, "peak_GBs": HBM_PEAK_GBS,
+            "hbm_frac": ALG_BYTES["bn254"] * bn.m / (bn_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "valu": valu_roofline(load_json("pmc_traffic.json"), load_json("r02_valu_mix.json"),
+                                  ["k_bn254_g1_decompress"], bn.m, bn_ms),
+            "verified_bit_exact": bn_ok, "rejected_points": 0 if bn_bad == KD.NO_BAD else 1, "generate_s": t_bn}
+        del bn
+        torch.cuda.empty_cache()
 
-    def step(record):
-        marks = []
-
-        def launch(op, comp, blocks, rin, out, rout, keys, c):
-            cnt = blocks[c][1]
-            src = comp[sum(x for _, x in blocks[:c]) * rin:][:cnt * rin]
-            e = [torch.cuda.Event(enable_timing=True) for _ in range(2)] if record else None
-            if record:
-                e[0].record()
-            D.codec_dev(op, src, dst_of(out, blocks, c, rout), keys[c:c + 1])
-            if record:
-                e[1].record()
-                marks.append((op, e))
-
-        if gather:
-            works = KD.decode_gather_pipelined(
-                lambda c, g0, dst: launch("g1_decompress", comp1, blocks1, 48, out1, 96, keys1, c),
-                out1, 96, n1, rank, world, len(blocks1))
-            works += KD.decode_gather_pipelined(
-                lambda c, g0, dst: launch("g2_decompress", comp2, blocks2, 96, out2, 192, keys2, c),
-                out2, 192, n2, rank, world, len(blocks2))
-            for w in works:
-                w.wait()  # the current stream waits for the collectives
-        else:
-            for c in range(len(blocks1)):
-                launch("g1_decompress", comp1, blocks1, 48, out1, 96, keys1, c)
-            for c in range(len(blocks2)):
-                launch("g2_decompress", comp2, blocks2, 96, out2, 192, keys2, c)
-        if record:
-            ev.append(marks)
-
-    def bad_key():
-        ks = [KD.key_with_offset(D.read_key(keys1[c:c + 1]), blocks1[c][0]) for c in range(len(blocks1))]
-        ks += [KD.key_with_offset(D.read_key(keys2[c:c + 1]), blocks2[c][0]) for c in range(len(blocks2))]
-        return min(ks)
-
-    for _ in range(args.warmup):
-        step(False)
-    torch.cuda.synchronize()
-
-    verified = None
-    if not args.no_verify:
-        if args.warmup == 0:
-            step(False)
-            torch.cuda.synchronize()
-        ok = bad_key() == KD.NO_BAD
-        for out, blocks, exps, rec in ((out1, blocks1, exp1, 96), (out2, blocks2, exp2, 192)):
-            for c, e in enumerate(exps):
-                ok = ok and torch.equal(dst_of(out, blocks, c, rec), e)
-            if gather:  # blocks decoded by the other ranks: per-block checksums against their owners'
-                nb = out.numel() // (blocks[0][1] * rec)
-                mine = torch.zeros(nb, 2, dtype=torch.int64, device=dev)
-                w = torch.arange(1, blocks[0][1] * rec // 8 + 1, dtype=torch.int64, device=dev)
-                for (g0, cnt), e in zip(blocks, exps):
-                    v = e.view(torch.int64)
-                    mine[g0 // cnt] = torch.stack([v.sum(), (v * w).sum()])
-                dist.all_reduce(mine)  # each block has exactly one owner
-                got = out.view(torch.int64).view(nb, -1)
-                ok = ok and torch.equal(torch.stack([got.sum(1), (got * w).sum(1)], 1), mine)
-        if world > 1:
-            t = torch.tensor([1 if ok else 0], device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MIN)
-            ok = bool(t.item())
-        verified = bool(ok)
-        del exp1, exp2
-
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(True)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        bad = KD.allreduce_min_key(bad_key(), dev)
-    else:
-        bad = bad_key()
-
-    # SURVEY §8f row 2 (loader mirror), measured after the timed region on rank 0: the G1 ark
-    # records just produced -> in-memory GroupAffine (deserialize_unchecked), HBM-bound.
-    next_rows = None
-    if rank == 0 and not args.no_next_rows:
+    # SURVEY §8f rows, measured after the timed region on rank 0 only
+    if next_rows is not None and rank == 0:
+        m1 = g1.m
+        rec1 = g1.out[:m1 * 96]  # m1 G1 ark records (any of them: all decoded and verified)
+        # row 2 (loader mirror): the G1 ark records just produced -> in-memory GroupAffine
+        # (deserialize_unchecked), HBM-bound
         outl = torch.empty(m1 * 104, dtype=torch.uint8, device=dev)
         keyl = torch.empty(1, dtype=torch.int64, device=dev)
-        rec1 = out1[:m1 * 96]  # m1 G1 ark records (any of them: all decoded and verified)
         D.codec_dev("g1_load", rec1, outl, keyl)
         le = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         le[0].record()
@@ -338,14 +479,14 @@ def main():
         torch.cuda.synchronize()
         load_ms = le[0].elapsed_time(le[1]) / 5
         load_gbs = 200 * m1 / (load_ms * 1e-3) / 1e9
-        next_rows = {"g1_deserialize_unchecked": {
+        next_rows["g1_deserialize_unchecked"] = {
             "kernel": "k_g1_load (load_kzg_setup per-point work)", "points": m1, "launch_ms": load_ms,
             "points_per_s": m1 / (load_ms * 1e-3), "algorithmic_bytes_per_point": 200,
             "achieved_GBs": load_gbs, "peak_GBs": HBM_PEAK_GBS, "hbm_frac": load_gbs / HBM_PEAK_GBS,
-            "all_accepted": D.read_key(keyl) == KD.NO_BAD}}
+            "all_accepted": D.read_key(keyl) == KD.NO_BAD}
         del outl
-        # SURVEY §8f row 3 (uncompressed-input mode, the read_g1 loop alone): pairing-uncompressed
-        # records = per-coordinate byte reversal of the ark records (A6 identity); decode them back
+        # row 3 (uncompressed-input mode, the read_g1 loop alone): pairing-uncompressed records =
+        # per-coordinate byte reversal of the ark records (A6 identity); decode them back
         nt = min(m1, 1 << 24)
         ark = rec1[:nt * 96]
         pin = ark.view(nt, 2, 48).flip(-1).contiguous().view(-1)
@@ -384,50 +525,23 @@ def main():
             "workload": "config 3: 2^20 G1 + 2^20 G2 compressed -> ark uncompressed, subgroup-checked, 1 GPU",
             "g1_ms": g1c, "g2_ms": g2c, "points_per_s": 2 * n3 / ((g1c + g2c) * 1e-3),
             "g2_ns_per_point": g2c * 1e6 / n3,
+            "g2_valu": valu_roofline(load_json("pmc_traffic.json"), load_json("r02_valu_mix.json"),
+                                     ["k_g2_decompress", "k_g2_check"], n3, g2c),
             "verified_bit_exact": bool(D.read_key(k3[0:1]) == KD.NO_BAD and D.read_key(k3[1:2]) == KD.NO_BAD
                                        and torch.equal(o31, x31) and torch.equal(o32, x32))}
         del c31, x31, c32, x32, o31, o32
-        # BN254 G1, ark compressed (32 B) -> uncompressed (64 B)
-        if args.bn254_log2 > 0:
-            nb = 1 << args.bn254_log2
-            t_bn = time.perf_counter()
-            compb, expb = D.synth("bn254", args.seed + 2, 0, nb, dev, with_expected=True)
-            torch.cuda.synchronize()
-            t_bn = time.perf_counter() - t_bn
-            outb = torch.empty(nb * 64, dtype=torch.uint8, device=dev)
-            keyb = torch.empty(1, dtype=torch.int64, device=dev)
-            D.codec_dev("bn254_g1_decompress", compb, outb, keyb)  # warm-up, verified below
-            be = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-            be[0].record()
-            for _ in range(3):
-                D.codec_dev("bn254_g1_decompress", compb, outb, keyb)
-            be[1].record()
-            torch.cuda.synchronize()
-            bn_ms = be[0].elapsed_time(be[1]) / 3
-            ok = D.read_key(keyb) == KD.NO_BAD and torch.equal(outb, expb)
-            next_rows["bn254_g1_decompress"] = {
-                "workload": f"config 5: 2^{args.bn254_log2} BN254 G1, ark compressed 32 B -> ark uncompressed 64 B",
-                "kernel": "k_bn254_g1_decompress", "points": nb, "launch_ms": bn_ms,
-                "points_per_s": nb / (bn_ms * 1e-3), "algorithmic_bytes_per_point": 96,
-                "achieved_GBs": 96 * nb / (bn_ms * 1e-3) / 1e9, "peak_GBs": HBM_PEAK_GBS,
-                "hbm_frac": 96 * nb / (bn_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                "verified_bit_exact": bool(ok), "generate_s": t_bn}
-            del compb, expb, outb
-        # end-to-end preprocess (host transcript in → host kgz / fastkzg file
-        # out, PCIe both ways, BLAKE2b of both on host threads) at the reference's N = 2^21
+        # row 1: end-to-end preprocess (host transcript in -> host kgz / fastkzg file out, PCIe both
+        # ways, BLAKE2b of both on host threads) at the reference's N = 2^21, buffers and files
         if world == 1 and args.e2e_log2 > 0:
             next_rows.update(e2e_preprocess(args.e2e_log2, args.seed + 3, dev, kzgpot, D))
 
-    g1_ms = sum(e[0].elapsed_time(e[1]) for marks in ev for op, e in marks if op == "g1_decompress") / len(ev)
-    g2_ms = sum(e[0].elapsed_time(e[1]) for marks in ev for op, e in marks if op == "g2_decompress") / len(ev)
     ms_per_step = elapsed * 1e3 / args.steps
     value = (n1 + n2) * args.steps / elapsed
 
     result = None
     if rank == 0:
-        achieved = ALG_BYTES_G1 * m1 / (g1_ms * 1e-3) / 1e9
-        pmc = pmc_profile()
-        traffic = pmc_traffic(pmc, m1)
+        achieved = ALG_BYTES["g1"] * g1.m / (g1_ms * 1e-3) / 1e9
+        pmc = load_json("pmc_traffic.json")
         result = {
             "metric": "G1+G2 points decompressed+checked/sec, 2^27 BLS12-381 PoT",
             "value": value,
@@ -456,21 +570,25 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
-                "traffic": traffic,
+                "traffic": pmc_traffic(pmc, g1.m),
                 "launch_ms": g1_ms,
-                "algorithmic_bytes_per_point": ALG_BYTES_G1,
+                "algorithmic_bytes_per_point": ALG_BYTES["g1"],
                 "note": "integer-VALU bound, not HBM: see valu",
             },
-            "valu": valu_roofline(pmc, m1, g1_ms),
+            "valu": valu_roofline(pmc, load_json("r02_valu_mix.json"), ["k_g1_decompress", "k_g1_check"], g1.m, g1_ms),
             "kernels_ms": {"g1_codec": g1_ms, "g2_codec": g2_ms},
             "verified_bit_exact": verified,
+            "oracle_sample_check": sample,
             "rejected_points": 0 if bad == KD.NO_BAD else 1,
             "generate_s": t_gen,
         }
         if next_rows:
             result["next_rows"] = next_rows
         if world == 1 and not args.no_cpu_baseline:
-            result["cpu_baseline"] = cpu_baseline(comp1, comp2, args.cpu_sample_log2)
+            result["cpu_baseline"] = cpu_baseline(g1.comp if hasattr(g1, "comp") else
+                                                  D.synth("g1", args.seed, 0, 1 << args.cpu_sample_log2, dev,
+                                                          with_expected=False)[0],
+                                                  g2.comp, args.cpu_sample_log2)
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.barrier()

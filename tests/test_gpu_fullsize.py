@@ -41,6 +41,32 @@ def test_config4_round_trip_full_size(dev):
     assert 0.45 < frac < 0.55
 
 
+def test_config4_output_sampled_by_oracle(dev, oracle_lib):
+    """The generator shares fp381.hpp / curve.hpp with the codec, so the round trip above cannot
+    see a bug in a primitive both use. Here 64 runs of 256 records spread over the whole 2^27-point
+    output, plus its last 256 records (beyond the 4 GiB output offset), are decoded independently
+    by the C oracle (the reference's algorithms: Fq sqrt by a^((p-3)/4), ark mul_bits(r)) from the
+    same compressed inputs; bytes and accept/reject must match."""
+    torch, D = dev
+    cuda = torch.device("cuda", 0)
+    n1 = 1 << 27
+    comp1, _ = D.synth("g1", 10, 0, n1, cuda, with_expected=False)
+    out1 = torch.empty(n1 * 96, dtype=torch.uint8, device=cuda)
+    key = torch.empty(1, dtype=torch.int64, device=cuda)
+    D.codec_dev("g1_decompress", comp1, out1, key)
+    assert D.read_key(key) == (1 << 64) - 1
+    starts = [k * (n1 // 64) for k in range(64)] + [n1 - 256]
+    c = comp1.view(-1, 48)
+    o = out1.view(-1, 96)
+    data = b"".join(bytes(c[s:s + 256].cpu().numpy()) for s in starts)
+    got = b"".join(bytes(o[s:s + 256].cpu().numpy()) for s in starts)
+    n = 256 * len(starts)
+    want, st, fb, r = oracle_run(oracle_lib, "g1_decompress", data, n, threads=16)
+    assert r == 0 and fb == -1 and st == bytes(n)
+    assert got == want
+    assert (n1 - 1) * 96 > 1 << 32  # the last run lies past the 4 GiB output offset
+
+
 def test_generator_matches_oracle(dev, oracle_lib):
     torch, D = dev
     cuda = torch.device("cuda", 0)
