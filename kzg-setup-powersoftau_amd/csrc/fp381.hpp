@@ -172,6 +172,12 @@ KZG_DEV void fp_subk_nr(Fe<Tr>& r, const Fe<Tr>& a, const Fe<Tr>& b, const uint3
 #pragma unroll
   for (int i = 0; i < Tr::NL; i++) r.v[i] = (a.v[i] + k[i]) - b.v[i];
 }
+// r = K - b (the additive inverse of b, as a borrowed multiple K of p minus b, limb by limb)
+template <class Tr>
+KZG_DEV void fp_negk_nr(Fe<Tr>& r, const Fe<Tr>& b, const uint32_t (&k)[Tr::NL]) {
+#pragma unroll
+  for (int i = 0; i < Tr::NL; i++) r.v[i] = k[i] - b.v[i];
+}
 // carry-propagate to 28-bit limbs (value unchanged; top limb keeps the excess)
 template <class Tr>
 KZG_DEV void fp_norm(Fe<Tr>& r, const Fe<Tr>& a) {

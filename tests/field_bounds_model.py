@@ -284,24 +284,21 @@ class Field:
 # ------------------------------------------------------------------------------------------
 # formulas (mirror csrc/curve.hpp)
 def jac_dbl_fp(X, Y, Z):
-    """jac_dbl(jac<fp>&) — the hot path."""
+    """jac_dbl(jac<fp>&) — the hot path (Y3 = E (D - X3) + B (-8B) in one reduction)."""
     a = sqr(X, "A")
     b = sqr(Y, "B")
-    t = shl(b, 1)
-    c4 = sqr(t, "4C")
     t = shl(X, 2)
     d = mul(t, b, "D")
     e = mul3(a)
     t = shl(Y, 1)
     z3 = mul(t, Z, "Z3")
-    a = sqr(e, "F")
+    f = sqr(e, "F")
     t = shl(d, 1)
-    x3 = subk(a, t, "KB_8_29", "X3")
+    x3 = subk(f, t, "KB_8_29", "X3")
     t = mul3(d)
-    t = subk(t, a, "KB_8_28", "3D-F")
-    t = mul(e, t, "E(D-X3)")
-    c8 = shl(c4, 1)
-    y3 = subk(t, c8, "KB_8_29", "Y3")
+    t = subk(t, f, "KB_8_28", "3D-F")
+    n = norm(subk(normalized(0), shl(b, 3), "KB_64_31", "-8B"), "-8B")
+    y3 = mul_sum2(e, t, b, n, "Y3")
     return x3, y3, z3
 
 
