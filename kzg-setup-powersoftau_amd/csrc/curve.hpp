@@ -53,6 +53,19 @@ KZG_DEV void f_mul3(fp2& r, const fp2& a) {
   fp_add_red(r.c1, t.c1, a.c1);
 }
 KZG_DEV void f_norm(fp2& r, const fp2& a) { r = a; }
+// r = a b - c d. Fp: one reduction for both products (d negated as a borrowed multiple of p);
+// Fp2: two multiplies and a reduced subtraction.
+KZG_DEV void f_mul_sub(fp& r, const fp& a, const fp& b, const fp& c, const fp& d) {
+  fp nd;
+  fp_negk_nr(nd, d, BlsFp::KB_4_28);
+  fp_mul_sum2(r, a, b, c, nd);
+}
+KZG_DEV void f_mul_sub(fp2& r, const fp2& a, const fp2& b, const fp2& c, const fp2& d) {
+  fp2 t, u;
+  f_mul(t, a, b);
+  f_mul(u, c, d);
+  f_subk(r, t, u, BlsFp::KB_32_28);
+}
 
 // ---------------------------------------------------------------- doubling
 // Hot path (G1, 126 doublings per point). In: X, Y limbs < 2^30, Z normalized, values <= 110.
@@ -161,12 +174,9 @@ KZG_DEV void jac_madd(jac<F>& p, Load&& load) {
   f_norm(hh, hh);              // V - X3
   f_shl<1>(r, r);
   f_norm(r, r);                // r = 2 r'
-  f_mul(hh, r, hh);            // r (V - X3)
   f_shl<1>(h, p.y);
-  f_norm(h, h);
-  f_mul(j, h, j);              // 2 Y1 J
-  f_subk(p.y, hh, j, BlsFp::KB_32_28);
-  f_norm(p.y, p.y);            // Y3
+  f_norm(h, h);                // 2 Y1
+  f_mul_sub(p.y, r, hh, h, j); // Y3 = r (V - X3) - 2 Y1 J
   p.x = t;
 }
 

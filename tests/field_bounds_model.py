@@ -254,6 +254,12 @@ class Field:
             return V2(sub_red(a.c0, b.c0, name), sub_red(a.c1, b.c1, name))
         return subk(a, b, k, name)
 
+    def mul_sub(self, a, b, c, d, name="mul_sub"):
+        """f_mul_sub: a b - c d (Fp: mul_sum2 with d negated against KB_4_28)."""
+        if self.two:
+            return self.subk(self.mul(a, b, name), self.mul(c, d, name), "KB_32_28", name)
+        return mul_sum2(a, b, c, subk(normalized(0), d, "KB_4_28", name + ".nd"), name)
+
     def shl(self, a, s, name="shl"):
         if self.two:
             for _ in range(s):
@@ -348,10 +354,8 @@ def jac_madd(F, X, Y, Z, x2, y2):
     t = F.norm(F.subk(t, h2, "KB_64_29", "X3"))
     hh = F.norm(F.subk(hh, t, "KB_128_28", "V-X3"))
     r = F.norm(F.shl(r, 1))
-    hh = F.mul(r, hh, "r(V-X3)")
     h = F.norm(F.shl(Y, 1))
-    j = F.mul(h, j, "2Y1J")
-    y3 = F.norm(F.subk(hh, j, "KB_32_28", "Y3"))
+    y3 = F.mul_sub(r, hh, h, j, "Y3")  # r (V - X3) - 2 Y1 J
     one = F.one()
     jn = (lambda a, b: V2(vmax(a.c0, b.c0), vmax(a.c1, b.c1))) if F.two else vmax
     return jn(jn(t, xd), x2), jn(jn(y3, yd), y2), jn(jn(z3, zd), one)
