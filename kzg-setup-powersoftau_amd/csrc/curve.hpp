@@ -25,46 +25,17 @@ struct jac {
 };
 
 // ---------------------------------------------------------------- generic helpers
-// Fp: carry-free limb-wise forms (bounds proven by tests/test_field_bounds.py).
-// Fp2 (cold G2 path): every component stays reduced (< 2p); the borrowed constant is not needed
-// and each op reduces its result, so the same formulas hold with no value drift.
+// Fp forms used by the generic jac_madd / jac_eq_affine (instantiated for Fp; the G2 ladders
+// have their own carry-free Fp2 overloads below): carry-free limb-wise forms, bounds proven by
+// tests/test_field_bounds.py.
 KZG_DEV void f_subk(fp& r, const fp& a, const fp& b, const uint32_t (&k)[NL]) { fp_subk_nr(r, a, b, k); }
-KZG_DEV void f_subk(fp2& r, const fp2& a, const fp2& b, const uint32_t (&)[NL]) {
-  fp_sub_red(r.c0, a.c0, b.c0);
-  fp_sub_red(r.c1, a.c1, b.c1);
-}
 template <int S>
 KZG_DEV void f_shl(fp& r, const fp& a) { fp_shl_nr<S>(r, a); }
-template <int S>
-KZG_DEV void f_shl(fp2& r, const fp2& a) {
-  r = a;
-#pragma unroll
-  for (int k = 0; k < S; k++) {
-    fp_add_red(r.c0, r.c0, r.c0);
-    fp_add_red(r.c1, r.c1, r.c1);
-  }
-}
-KZG_DEV void f_mul3(fp& r, const fp& a) { fp_mul3_nr(r, a); }
-KZG_DEV void f_mul3(fp2& r, const fp2& a) {
-  fp2 t;
-  fp_add_red(t.c0, a.c0, a.c0);
-  fp_add_red(t.c1, a.c1, a.c1);
-  fp_add_red(r.c0, t.c0, a.c0);
-  fp_add_red(r.c1, t.c1, a.c1);
-}
-KZG_DEV void f_norm(fp2& r, const fp2& a) { r = a; }
-// r = a b - c d. Fp: one reduction for both products (d negated as a borrowed multiple of p);
-// Fp2: two multiplies and a reduced subtraction.
+// r = a b - c d in one reduction (d negated as a borrowed multiple of p)
 KZG_DEV void f_mul_sub(fp& r, const fp& a, const fp& b, const fp& c, const fp& d) {
   fp nd;
   fp_negk_nr(nd, d, BlsFp::KB_4_28);
   fp_mul_sum2(r, a, b, c, nd);
-}
-KZG_DEV void f_mul_sub(fp2& r, const fp2& a, const fp2& b, const fp2& c, const fp2& d) {
-  fp2 t, u;
-  f_mul(t, a, b);
-  f_mul(u, c, d);
-  f_subk(r, t, u, BlsFp::KB_32_28);
 }
 
 // ---------------------------------------------------------------- doubling
@@ -93,34 +64,117 @@ KZG_DEV void jac_dbl(jac<fp>& p) {
   fp_mul_sum2(p.y, e, t, b, n);  // Y3 = E (D - X3) + B (-8B)  N
 }
 
-// Generic (Fp2, cold): all values reduced (< 2p) through the Fp2 helpers above. Ordered so
-// that each input dies as early as possible (Y after B and Z3, X after A and D): at most five
-// Fp2 temporaries live beside the Karatsuba scratch, which keeps the G2 kernels off AGPR spills.
-template <typename F>
-KZG_DEV void jac_dbl(jac<F>& p) {
-  F b, t, a, d, c8;
-  f_sqr(b, p.y);               // B = Y^2
-  f_shl<1>(t, p.y);
-  f_norm(t, t);
-  f_mul(p.z, t, p.z);          // Z3 = 2YZ           (Y dead)
-  f_sqr(a, p.x);               // A = X^2
-  f_shl<2>(t, p.x);
-  f_norm(t, t);
-  f_mul(d, t, b);              // D = 4XB            (X dead)
-  f_shl<3>(t, b);
-  f_norm(t, t);
-  f_mul(c8, t, b);             // 8C = 8B^2          (B dead)
-  f_mul3(a, a);
-  f_norm(a, a);                // E = 3A             (A dead)
-  f_sqr(t, a);                 // F = E^2
-  f_shl<1>(p.y, d);
-  f_subk(p.x, t, p.y, BlsFp::KB_64_29);
-  f_norm(p.x, p.x);            // X3 = F - 2D        (F dead)
-  f_subk(t, d, p.x, BlsFp::KB_128_28);
-  f_norm(t, t);                // D - X3            (D dead)
-  f_mul(t, a, t);
-  f_subk(p.y, t, c8, BlsFp::KB_32_28);
-  f_norm(p.y, p.y);            // Y3 = E (D - X3) - 8C
+// ---------------------------------------------------------------- Fp2, carry-free (G2 ladders)
+// The G1 discipline on both components: limb-wise adds and borrowed-constant subtractions, an
+// fp_norm only where the next multiply needs normalized limbs — instead of the reduced (< 2p)
+// helpers' serial borrow / carry / conditional-2p chains (~125 instructions each, 24 per
+// doubling). Every constant is the one tests/field_bounds_model.py (jac_dbl_fp2_lz,
+// jac_madd_fp2_lz, jac_eq_affine_fp2_lz) proves for all inputs; ladder states stay normalized
+// with values below ~21 p.
+// r = a b with b.c1 negated against k (k must dominate b.c1): two Montgomery reductions
+KZG_DEV void f2_mul_lz(fp2& r, const fp2& a, const fp2& b, const uint32_t (&k)[NL]) {
+  fp nb1, c0;
+  fp_negk_nr(nb1, b.c1, k);
+  fp_mul_sum2(c0, a.c0, b.c0, a.c1, nb1);
+  fp_mul_sum2(r.c1, a.c0, b.c1, a.c1, b.c0);
+  r.c0 = c0;
+}
+// r = a^2 = (a0 + a1)(a0 - a1) + 2 a0 a1 u, the difference against k (dominating a.c1)
+KZG_DEV void f2_sqr_lz(fp2& r, const fp2& a, const uint32_t (&k)[NL]) {
+  fp s, d, t;
+  fp_add_nr(s, a.c0, a.c1);
+  fp_subk_nr(d, a.c0, a.c1, k);
+  fp_shl_nr<1>(t, a.c0);
+  fp_mul(r.c1, t, a.c1);
+  fp_mul(r.c0, s, d);
+}
+KZG_DEV void f2_subk(fp2& r, const fp2& a, const fp2& b, const uint32_t (&k)[NL]) {
+  fp_subk_nr(r.c0, a.c0, b.c0, k);
+  fp_subk_nr(r.c1, a.c1, b.c1, k);
+}
+template <int S>
+KZG_DEV void f2_shl(fp2& r, const fp2& a) {
+  fp_shl_nr<S>(r.c0, a.c0);
+  fp_shl_nr<S>(r.c1, a.c1);
+}
+KZG_DEV void f2_norm(fp2& r, const fp2& a) {
+  fp_norm(r.c0, a.c0);
+  fp_norm(r.c1, a.c1);
+}
+
+// G2 doubling (63 per point): X, Y, Z normalized in and out. 4 squarings + 3 multiplies in Fp2.
+KZG_DEV void jac_dbl(jac<fp2>& p) {
+  fp2 b, a, d, t;
+  f2_sqr_lz(b, p.y, BlsFp::KB_32_28);        // B = Y^2
+  f2_shl<1>(t, p.y);
+  f2_mul_lz(p.z, t, p.z, BlsFp::KB_16_28);   // Z3 = 2 Y Z          (Y dead)
+  f2_sqr_lz(a, p.x, BlsFp::KB_16_28);        // A = X^2
+  f2_shl<2>(t, p.x);
+  f2_mul_lz(d, t, b, BlsFp::KB_2_28);        // D = 4 X B           (X dead)
+  f2_sqr_lz(b, b, BlsFp::KB_2_28);           // C = B^2             (B dead)
+  fp_mul3_nr(a.c0, a.c0);
+  fp_mul3_nr(a.c1, a.c1);
+  f2_norm(a, a);                             // E = 3 A             (A dead)
+  f2_sqr_lz(t, a, BlsFp::KB_4_28);           // F = E^2
+  f2_shl<1>(p.x, d);
+  f2_subk(p.x, t, p.x, BlsFp::KB_4_29);
+  f2_norm(p.x, p.x);                         // X3 = F - 2D         (F dead)
+  f2_subk(d, d, p.x, BlsFp::KB_8_28);        // D - X3
+  f2_mul_lz(t, a, d, BlsFp::KB_16_30);       // E (D - X3)
+  f2_shl<3>(b, b);                           // 8C
+  f2_subk(p.y, t, b, BlsFp::KB_16_31);
+  f2_norm(p.y, p.y);                         // Y3 = E (D - X3) - 8C
+}
+
+// G2 mixed addition (ark add_assign_mixed incl. its zero / equal-point branches, as jac_madd):
+// X, Y, Z normalized in and out; the base point (x2, y2) normalized, values < 1.01 p.
+template <typename Load>
+KZG_DEV void jac_madd(jac<fp2>& p, Load&& load) {
+  fp2 z1z1, h, r, t;
+  {
+    fp2 x2, y2;
+    load(x2, y2);
+    f2_sqr_lz(z1z1, p.z, BlsFp::KB_2_28);
+    f2_mul_lz(h, x2, z1z1, BlsFp::KB_2_28);  // U2
+    f2_subk(h, h, p.x, BlsFp::KB_32_28);
+    f2_norm(h, h);                           // H = U2 - X1
+    f2_mul_lz(t, y2, p.z, BlsFp::KB_2_28);
+    f2_mul_lz(t, t, z1z1, BlsFp::KB_2_28);   // S2
+    f2_subk(r, t, p.y, BlsFp::KB_32_28);
+    f2_norm(r, r);                           // r' = S2 - Y1   (ark's r = 2 r')
+  }
+  const bool z1zero = f_is_zero(p.z);
+  const bool same = !z1zero && f_is_zero(h) && f_is_zero(r);
+  if (__builtin_expect(z1zero || same, 0)) {
+    if (same) {
+      jac_dbl(p);
+    } else {
+      load(p.x, p.y);
+      f_one(p.z);
+    }
+    return;
+  }
+  fp2 hh, j;
+  f2_sqr_lz(hh, h, BlsFp::KB_64_28);         // HH
+  f2_shl<1>(t, p.z);
+  f2_mul_lz(p.z, t, h, BlsFp::KB_64_28);     // Z3 = 2 Z1 H
+  f2_shl<2>(hh, hh);                         // I = 4 HH
+  f2_mul_lz(j, h, hh, BlsFp::KB_8_30);       // J = H I
+  f2_mul_lz(hh, p.x, hh, BlsFp::KB_8_30);    // V = X1 I
+  f2_sqr_lz(t, r, BlsFp::KB_64_28);          // r'^2
+  f2_shl<2>(t, t);                           // r^2 = 4 r'^2
+  f2_subk(t, t, j, BlsFp::KB_2_28);
+  f2_shl<1>(h, hh);                          // 2V
+  f2_subk(t, t, h, BlsFp::KB_4_29);
+  f2_norm(t, t);                             // X3 = r^2 - J - 2V
+  f2_subk(hh, hh, t, BlsFp::KB_32_28);       // V - X3
+  f2_shl<1>(r, r);                           // r = 2 r'
+  f2_mul_lz(hh, r, hh, BlsFp::KB_64_30);     // r (V - X3)
+  f2_shl<1>(h, p.y);                         // 2 Y1
+  f2_mul_lz(j, h, j, BlsFp::KB_2_28);        // 2 Y1 J
+  f2_subk(p.y, hh, j, BlsFp::KB_4_28);
+  f2_norm(p.y, p.y);                         // Y3 = r (V - X3) - 2 Y1 J
+  p.x = t;
 }
 
 // ---------------------------------------------------------------- mixed addition (cold)
@@ -202,6 +256,20 @@ KZG_DEV bool jac_eq_affine(const jac<F>& p, const F& x, const F& y) {
   f_mul(z2, z2, p.z);
   f_mul(t, y, z2);
   f_subk(t, t, p.y, BlsFp::KB_128_31);
+  ok = ok && f_is_zero(t);
+  return ok && !f_is_zero(p.z);
+}
+
+// The same test on a carry-free G2 ladder state; x, y reduced or normalized with value < 1.01 p.
+KZG_DEV bool jac_eq_affine(const jac<fp2>& p, const fp2& x, const fp2& y) {
+  fp2 z2, t;
+  f2_sqr_lz(z2, p.z, BlsFp::KB_2_28);
+  f2_mul_lz(t, x, z2, BlsFp::KB_2_28);
+  f2_subk(t, t, p.x, BlsFp::KB_32_28);
+  bool ok = f_is_zero(t);
+  f2_mul_lz(z2, z2, p.z, BlsFp::KB_2_28);
+  f2_mul_lz(t, y, z2, BlsFp::KB_2_28);
+  f2_subk(t, t, p.y, BlsFp::KB_32_28);
   ok = ok && f_is_zero(t);
   return ok && !f_is_zero(p.z);
 }

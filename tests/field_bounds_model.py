@@ -308,28 +308,8 @@ def jac_dbl_fp(X, Y, Z):
     return x3, y3, z3
 
 
-def jac_dbl_generic(F, X, Y, Z):
-    """curve.hpp jac_dbl<F> (the Fp2 instantiation; every op reduces)."""
-    b = F.sqr(Y, "B")
-    t = F.norm(F.shl(Y, 1))
-    z3 = F.mul(t, Z, "Z3")
-    a = F.sqr(X, "A")
-    t = F.norm(F.shl(X, 2))
-    d = F.mul(t, b, "D")
-    t = F.norm(F.shl(b, 3))
-    c8 = F.mul(t, b, "8C")
-    e = F.norm(F.mul3(a))
-    f = F.sqr(e, "F")
-    t2 = F.shl(d, 1)
-    x3 = F.norm(F.subk(f, t2, "KB_64_29", "X3"))
-    t = F.norm(F.subk(d, x3, "KB_128_28", "D-X3"))
-    t = F.mul(e, t, "E(D-X3)")
-    y3 = F.norm(F.subk(t, c8, "KB_32_28", "Y3"))
-    return x3, y3, z3
-
-
 def jac_dbl(F, X, Y, Z):
-    return jac_dbl_generic(F, X, Y, Z) if F.two else jac_dbl_fp(X, Y, Z)
+    return jac_dbl_fp2_lz(X, Y, Z) if F.two else jac_dbl_fp(X, Y, Z)
 
 
 def jac_madd(F, X, Y, Z, x2, y2):
@@ -423,3 +403,126 @@ def ladder_invariant(F, base_x, base_y, rounds=12):
     else:
         raise BoundError("ladder bound set is not closed: values keep growing")
     return S
+
+
+# ------------------------------------------------------------------------------------------
+# Fp2 in the carry-free ("lazy") discipline of the G1 path — the G2 ladders (curve.hpp
+# jac_dbl(jac<fp2>&), jac_madd(jac<fp2>&, ..), jac_eq_affine(jac<fp2>, ..)). Each component is
+# a V with its own limb / value bounds, exactly as for Fp.
+def mul2(a: V2, b: V2, kname, name="mul2"):
+    """f2_mul_lz: c0 = REDC(a0 b0 + a1 (K - b1)), c1 = REDC(a0 b1 + a1 b0)."""
+    nb1 = subk(normalized(0), b.c1, kname, name + ".nb1")
+    return V2(mul_sum2(a.c0, b.c0, a.c1, nb1, name + ".c0"), mul_sum2(a.c0, b.c1, a.c1, b.c0, name + ".c1"))
+
+
+def sqr2(a: V2, kname, name="sqr2"):
+    """f2_sqr_lz: c0 = REDC((a0 + a1)(a0 + K - a1)), c1 = REDC(2 a0 a1)."""
+    s = add_nr(a.c0, a.c1, name + ".s")
+    d = subk(a.c0, a.c1, kname, name + ".d")
+    return V2(mul(s, d, name + ".c0"), mul(shl(a.c0, 1), a.c1, name + ".c1"))
+
+
+def subk2(a, b, kname, name="subk2"):
+    return V2(subk(a.c0, b.c0, kname, name + ".c0"), subk(a.c1, b.c1, kname, name + ".c1"))
+
+
+def norm2(a, name="norm2"):
+    return V2(norm(a.c0, name + ".c0"), norm(a.c1, name + ".c1"))
+
+
+def shl2(a, s, name="shl2"):
+    return V2(shl(a.c0, s, name), shl(a.c1, s, name))
+
+
+def mul3_2(a, name="mul3_2"):
+    return V2(mul3(a.c0, name), mul3(a.c1, name))
+
+
+def zero_ok2(a, name):
+    canon_ok(a.c0, name), canon_ok(a.c1, name)
+
+
+def jac_dbl_fp2_lz(X, Y, Z):
+    """curve.hpp jac_dbl(jac<fp2>&): X, Y, Z normalized in, normalized out."""
+    b = sqr2(Y, "KB_32_28", "B")
+    z3 = mul2(shl2(Y, 1), Z, "KB_16_28", "Z3")
+    a = sqr2(X, "KB_16_28", "A")
+    d = mul2(shl2(X, 2), b, "KB_2_28", "D")
+    e = norm2(mul3_2(a), "E")
+    f = sqr2(e, "KB_4_28", "F")
+    c = sqr2(b, "KB_2_28", "C")
+    x3 = norm2(subk2(f, shl2(d, 1), "KB_4_29", "X3"), "X3")
+    t = subk2(d, x3, "KB_8_28", "D-X3")
+    y3 = mul2(e, t, "KB_16_30", "E(D-X3)")
+    y3 = norm2(subk2(y3, shl2(c, 3), "KB_16_31", "Y3"), "Y3")
+    return x3, y3, z3
+
+
+def jac_madd_fp2_lz(X, Y, Z, x2, y2):
+    """curve.hpp jac_madd(jac<fp2>&, load): normalized in / out; base (x2, y2) normalized."""
+    z1z1 = sqr2(Z, "KB_2_28", "Z1Z1")
+    u2 = mul2(x2, z1z1, "KB_2_28", "U2")
+    h = norm2(subk2(u2, X, "KB_32_28", "H"), "H")
+    t = mul2(y2, Z, "KB_2_28", "y2Z")
+    s2 = mul2(t, z1z1, "KB_2_28", "S2")
+    r = norm2(subk2(s2, Y, "KB_32_28", "r'"), "r'")
+    zero_ok2(Z, "Z"), zero_ok2(h, "H"), zero_ok2(r, "r'")
+    xd, yd, zd = jac_dbl_fp2_lz(X, Y, Z)  # the equal-point branch
+    hh = sqr2(h, "KB_64_28", "HH")
+    z3 = mul2(shl2(Z, 1), h, "KB_64_28", "Z3m")
+    i = shl2(hh, 2, "I")
+    j = mul2(h, i, "KB_8_30", "J")
+    v = mul2(X, i, "KB_8_30", "V")
+    rr = sqr2(r, "KB_64_28", "r'^2")
+    x3 = subk2(shl2(rr, 2), j, "KB_2_28", "X3a")
+    x3 = norm2(subk2(x3, shl2(v, 1), "KB_4_29", "X3m"), "X3m")
+    vx = subk2(v, x3, "KB_32_28", "V-X3")
+    a = mul2(shl2(r, 1), vx, "KB_64_30", "r(V-X3)")
+    b = mul2(shl2(Y, 1), j, "KB_2_28", "2Y1J")
+    y3 = norm2(subk2(a, b, "KB_4_28", "Y3m"), "Y3m")
+    return (V2(vmax(x3.c0, xd.c0, x2.c0), vmax(x3.c1, xd.c1, x2.c1)),
+            V2(vmax(y3.c0, yd.c0, y2.c0), vmax(y3.c1, yd.c1, y2.c1)),
+            V2(vmax(z3.c0, zd.c0, normalized(1)), vmax(z3.c1, zd.c1, normalized(1))))
+
+
+def jac_eq_affine_fp2_lz(X, Y, Z, x, y):
+    """curve.hpp jac_eq_affine(const jac<fp2>&, ..): x Z^2 == X, y Z^3 == Y, Z != 0."""
+    z2 = sqr2(Z, "KB_2_28", "z2")
+    t = subk2(mul2(x, z2, "KB_2_28", "xZ2"), X, "KB_32_28", "eqx")
+    zero_ok2(t, "eqx")
+    z3 = mul2(z2, Z, "KB_2_28", "z3")
+    t = subk2(mul2(y, z3, "KB_2_28", "yZ3"), Y, "KB_32_28", "eqy")
+    zero_ok2(t, "eqy")
+    zero_ok2(Z, "Z")
+
+
+def ladder_invariant_fp2_lz(base_x, base_y, rounds=12):
+    """ladder_invariant for the lazy Fp2 ladder (mul_abs_u_affine / in_subgroup_ref over Fp2)."""
+    def join2(a, b):
+        return V2(vmax(a.c0, b.c0), vmax(a.c1, b.c1))
+
+    def infl(a):
+        return V2(_inflate1(a.c0, 1.01), _inflate1(a.c1, 1.01))
+
+    def within(a, b):
+        return all(all(x <= y for x, y in zip(u.limbs, w.limbs)) and u.val <= w.val
+                   for u, w in ((a.c0, b.c0), (a.c1, b.c1)))
+
+    def step(X, Y, Z):
+        outs = [jac_dbl_fp2_lz(X, Y, Z)]
+        outs.append(jac_madd_fp2_lz(*outs[0], base_x, base_y))
+        nx, ny, nz = X, Y, Z
+        for ox, oy, oz in outs:
+            nx, ny, nz = join2(nx, ox), join2(ny, oy), join2(nz, oz)
+        return nx, ny, nz
+
+    X, Y, Z = base_x, base_y, V2(normalized(1), normalized(0))
+    for _ in range(rounds):
+        X, Y, Z = step(X, Y, Z)
+    S = (infl(X), infl(Y), infl(Z))
+    for _ in range(40):
+        T = step(*S)
+        if all(within(a, b) for a, b in zip(T, S)):
+            return S
+        S = tuple(infl(join2(a, b)) for a, b in zip(T, S))
+    raise BoundError("lazy Fp2 ladder bound set is not closed")

@@ -11,11 +11,11 @@ import pytest
 import field_bounds_model as M
 
 
-@pytest.mark.parametrize("two", [False, True], ids=["fp", "fp2"])
-def test_ladders_closed(two):
+def test_ladders_closed():
+    """G1 ladders (the G2 ones: test_g2_lazy_ladder_closed)."""
+    two = False
     F = M.Field(two)
-    base = M.V2(M.normalized(Fraction(101, 100)), M.normalized(Fraction(101, 100))) if two else \
-        M.normalized(Fraction(101, 100))
+    base = M.normalized(Fraction(101, 100))
     S1 = M.ladder_invariant(F, base, base)                     # mul_abs_u_affine / in_subgroup_ref
     if not two:
         # G1 second ladder: Q1 = S1's (X, Y) is the affine base on the isomorphic curve; the
@@ -88,9 +88,39 @@ def test_fp2_sqrt_and_psi():
     py = M.V2(pm.c0, M.sub_red(M.normalized(0), pm.c1))
     py = M.f2_mul(py, M.V2(M.normalized(1), M.normalized(1)))
     py = M.V2(M.sub_red(M.normalized(0), py.c0), M.sub_red(M.normalized(0), py.c1))
-    F = M.Field(True)
-    S1 = M.ladder_invariant(F, pm, pm)
-    M.jac_eq_affine(F, *S1, px, py)
+    S1 = M.ladder_invariant_fp2_lz(pm, pm)
+    M.jac_eq_affine_fp2_lz(*S1, px, py)
+
+
+def test_g2_lazy_ladder_closed():
+    """G2 ladders (mul_abs_u_affine / in_subgroup_ref over Fp2) in the carry-free discipline:
+    curve.hpp jac_dbl(jac<fp2>&) / jac_madd(jac<fp2>&, ..) / jac_eq_affine(jac<fp2>, ..)."""
+    base = M.V2(M.normalized(Fraction(101, 100)), M.normalized(Fraction(101, 100)))
+    S = M.ladder_invariant_fp2_lz(base, base)
+    M.jac_eq_affine_fp2_lz(*S, base, base)
+    # psi(P) and -y are reduced (< 2p) values from the generic Fp2 helpers: within the same bound
+    red = M.V2(M.reduced(), M.reduced())
+    M.jac_eq_affine_fp2_lz(*S, red, red)
+
+
+def test_g2_synth_madd_chain_lazy():
+    """k_synth<fp2> (synth_kernels.hip): back-to-back lazy Fp2 mixed additions of table points,
+    then to_affine's reduced-discipline inverse and multiplies (inputs normalized, any value)."""
+    base = M.V2(M.normalized(Fraction(101, 100)), M.normalized(Fraction(101, 100)))
+    S = (base, base, M.V2(M.normalized(1), M.normalized(0)))
+    for _ in range(40):
+        T = M.jac_madd_fp2_lz(*S, base, base)
+        T = tuple(M.V2(M.vmax(a.c0, b.c0), M.vmax(a.c1, b.c1)) for a, b in zip(S, T))
+        if all(M._within(M.Field(True), a, b) for a, b in zip(T, S)):
+            break
+        S = tuple(M.V2(M._inflate1(t.c0, 1.01), M._inflate1(t.c1, 1.01)) for t in T)
+    else:
+        raise AssertionError("lazy fp2 madd chain bound set not closed")
+    X, Y, Z = S
+    for c in (X.c0, X.c1, Y.c0, Y.c1):  # f_mul(x, p.x, z2) with z2 reduced: a mul_sum2 on normalized limbs
+        M.reduce_once_ok(M.mul_sum2(c, M.reduced(), c, M.subk(M.normalized(0), M.reduced(), "KB_4_28")))
+    for c in (Z.c0, Z.c1):  # f_inv: fp_sqr of each component, then a normalized sum
+        M.sqr(c)
 
 
 def test_bounds_model_catches_overflow():

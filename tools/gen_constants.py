@@ -28,7 +28,8 @@ NL = 14                 # limbs (BLS12-381)
 RM = 1 << (LB * NL)     # Montgomery R = 2^392
 W = 4                   # sqrt sliding window
 # (c, L) borrowed multiples used by the formulas in csrc/curve.hpp / fp381.hpp
-KB = [(2, 28), (4, 28), (8, 28), (8, 29), (16, 28), (32, 28), (32, 29), (64, 28), (64, 29), (64, 31), (128, 28), (128, 31)]
+KB = [(2, 28), (4, 28), (8, 28), (8, 29), (16, 28), (32, 28), (32, 29), (64, 28), (64, 29), (64, 31), (128, 28), (128, 31),
+      (4, 29), (8, 30), (16, 30), (64, 30), (16, 31)]  # the last five: the G2 ladders (curve.hpp, fp2)
 
 # BN254 base field (config 5; ark-bn254 0.2 Fq): 10 x 28-bit limbs, R = 2^280
 BN_P = 0x30644E72E131A029B85045B68181585D97816A916871CA8D3C208C16D87CFD47
