@@ -372,10 +372,11 @@ KZG_DEV void fp_from_mont(Fe<Tr>& canon, const Fe<Tr>& a) {
 // r = a^((p-3)/4): fixed sliding-window schedule (tools/gen_constants.py), identical for every
 // lane, so the whole wave follows one instruction stream. Loops stay rolled so one square and
 // one multiply body serve all operations (I-cache). Input limbs <= 2^30, output normalized.
-// The 8-entry table lives in scratch (per-lane private memory, cached): the wave-uniform lookup
-// is then 4 x 16-B loads, where a register-resident table needs a 224-instruction masked select
-// per lookup; measured 701 vs 752 ms for k_g1_decompress over 2^27 points (and the kernel drops
-// from 162 to 88 VGPRs).
+// The 8-entry table lives in registers, one 8-wide vector per limb read with a wave-uniform
+// index (below). An earlier scratch-memory table (per-lane private memory) was cheaper in
+// instructions but its per-CU working set overflowed L2 at full occupancy: 1,479 B/point of HBM
+// re-reads, against 71 B/point with the register table (PMC FETCH_SIZE, k_g1_decompress), and
+// 2,370 -> 2,343 ms per 2^27-point G1 codec pass.
 template <class Tr>
 KZG_DEV void fp_pow_pm3d4(Fe<Tr>& r, const Fe<Tr>& a) {
   static_assert(Tr::SQRT_TABLE == 8, "table held as one 8-wide register vector per limb");
