@@ -34,7 +34,7 @@
 
 namespace kzgpot {
 
-constexpr uint32_t LMASK = (1u << 28) - 1;
+constexpr uint32_t LMASK = (1u << 28) - 1;  // BLS12-381 limbs (BlsFp::MASK)
 
 template <class Tr>
 struct Fe {
@@ -75,13 +75,13 @@ KZG_DEV void fp_mul(Fe<Tr>& r, const Fe<Tr>& a, const Fe<Tr>& b) {
     if (i < N) {
       acc += (uint64_t)a.v[i] * b.v[0];
       acc += accp;
-      m[i] = ((uint32_t)acc * Tr::PINV) & LMASK;
+      m[i] = ((uint32_t)acc * Tr::PINV) & Tr::MASK;
       acc += (uint64_t)m[i] * Tr::P[0];
     } else {
       acc += accp;
-      r.v[i - N] = (uint32_t)acc & LMASK;
+      r.v[i - N] = (uint32_t)acc & Tr::MASK;
     }
-    acc >>= 28;
+    acc >>= Tr::LB;
   }
 }
 // r = (a b + c d) R^-1 mod p: both products and the m*p terms share one column scan and one
@@ -108,13 +108,13 @@ KZG_DEV void fp_mul_sum2(Fe<Tr>& r, const Fe<Tr>& a, const Fe<Tr>& b, const Fe<T
       acc += (uint64_t)a.v[i] * b.v[0];
       acc2 += (uint64_t)c.v[i] * d.v[0];
       acc += acc2 + accp;
-      m[i] = ((uint32_t)acc * Tr::PINV) & LMASK;
+      m[i] = ((uint32_t)acc * Tr::PINV) & Tr::MASK;
       acc += (uint64_t)m[i] * Tr::P[0];
     } else {
       acc += acc2 + accp;
-      r.v[i - N] = (uint32_t)acc & LMASK;
+      r.v[i - N] = (uint32_t)acc & Tr::MASK;
     }
-    acc >>= 28;
+    acc >>= Tr::LB;
   }
 }
 // r = a^2 R^-1 mod p: each cross product a_j a_k (j < k) once, as a_j (2 a_k), plus the squares —
@@ -140,14 +140,14 @@ KZG_DEV void fp_sqr(Fe<Tr>& r, const Fe<Tr>& a) {
     for (int k = j0; k <= k1; k++) accp += (uint64_t)m[k] * Tr::P[i - k];
     acc += accp;
     if (i < N) {
-      m[i] = ((uint32_t)acc * Tr::PINV) & LMASK;
+      m[i] = ((uint32_t)acc * Tr::PINV) & Tr::MASK;
       acc += (uint64_t)m[i] * Tr::P[0];
     } else {
-      r.v[i - N] = (uint32_t)acc & LMASK;
+      r.v[i - N] = (uint32_t)acc & Tr::MASK;
     }
-    acc >>= 28;
+    acc >>= Tr::LB;
   }
-  r.v[N - 1] = (uint32_t)acc & LMASK;  // column 2 NL - 1 holds only the carry
+  r.v[N - 1] = (uint32_t)acc & Tr::MASK;  // column 2 NL - 1 holds only the carry
 }
 
 // ------------------------------------------------------------------------------- limb-wise ops
@@ -185,8 +185,8 @@ KZG_DEV void fp_norm(Fe<Tr>& r, const Fe<Tr>& a) {
 #pragma unroll
   for (int i = 0; i < Tr::NL - 1; i++) {
     const uint32_t t = a.v[i] + c;
-    r.v[i] = t & LMASK;
-    c = t >> 28;
+    r.v[i] = t & Tr::MASK;
+    c = t >> Tr::LB;
   }
   r.v[Tr::NL - 1] = a.v[Tr::NL - 1] + c;
 }
@@ -203,8 +203,8 @@ KZG_DEV bool fp_sub_const_borrow(Fe<Tr>& d, const Fe<Tr>& a, const uint32_t (&k)
 #pragma unroll
   for (int i = 0; i < Tr::NL; i++) {
     const int32_t t = (int32_t)a.v[i] - (int32_t)k[i] + br;
-    d.v[i] = (uint32_t)t & LMASK;
-    br = t >> 28;  // arithmetic: 0 or -1
+    d.v[i] = (uint32_t)t & Tr::MASK;
+    br = t >> Tr::LB;  // arithmetic: 0 or -1
   }
   return br != 0;
 }
@@ -266,8 +266,8 @@ KZG_DEV bool fp_is_zero(const Fe<Tr>& a) {
 #pragma unroll
   for (int i = 0; i < N - 1; i++) {
     c += (uint64_t)k * Tr::P[i];
-    diff |= ((uint32_t)c & LMASK) ^ n.v[i];
-    c >>= 28;
+    diff |= ((uint32_t)c & Tr::MASK) ^ n.v[i];
+    c >>= Tr::LB;
   }
   c += (uint64_t)k * Tr::P[N - 1];
   diff |= (uint32_t)c ^ n.v[N - 1];
@@ -295,8 +295,8 @@ KZG_DEV void fp_neg_canon(Fe<Tr>& r, const Fe<Tr>& c) {
 #pragma unroll
   for (int i = 0; i < Tr::NL; i++) {
     const int32_t t = (int32_t)Tr::P[i] - (int32_t)c.v[i] + br;
-    r.v[i] = z ? 0u : ((uint32_t)t & LMASK);
-    br = t >> 28;
+    r.v[i] = z ? 0u : ((uint32_t)t & Tr::MASK);
+    br = t >> Tr::LB;
   }
 }
 
@@ -325,20 +325,20 @@ template <class Tr>
 KZG_DEV void fp_from_words(Fe<Tr>& r, const uint32_t (&w)[Tr::NW]) {
 #pragma unroll
   for (int k = 0; k < Tr::NL; k++) {
-    const int bit = 28 * k, i = bit >> 5, off = bit & 31;
+    const int bit = Tr::LB * k, i = bit >> 5, off = bit & 31;
     const uint32_t lo = i < Tr::NW ? w[i] >> off : 0u;
-    const uint32_t hi = (off > 4 && i + 1 < Tr::NW) ? (w[i + 1] << (32 - off)) : 0u;
-    r.v[k] = (lo | hi) & LMASK;
+    const uint32_t hi = (off > 32 - Tr::LB && i + 1 < Tr::NW) ? (w[i + 1] << (32 - off)) : 0u;
+    r.v[k] = (lo | hi) & Tr::MASK;
   }
 }
 template <class Tr>
 KZG_DEV void fp_to_words(uint32_t (&w)[Tr::NW], const Fe<Tr>& c) {  // c normalized, value < 2^(32 NW)
 #pragma unroll
   for (int j = 0; j < Tr::NW; j++) {
-    const int bit = 32 * j, k = bit / 28, off = bit % 28;
+    const int bit = 32 * j, k = bit / Tr::LB, off = bit % Tr::LB;
     uint32_t v = c.v[k] >> off;
-    if (k + 1 < Tr::NL) v |= c.v[k + 1] << (28 - off);
-    if (off > 24 && k + 2 < Tr::NL) v |= c.v[k + 2] << (56 - off);
+    if (k + 1 < Tr::NL) v |= c.v[k + 1] << (Tr::LB - off);
+    if (2 * Tr::LB - off < 32 && k + 2 < Tr::NL) v |= c.v[k + 2] << (2 * Tr::LB - off);
     w[j] = v;
   }
 }

@@ -34,16 +34,17 @@ def _load_consts(path=CONSTS):
 
 C = _load_consts()
 
-FIELDS = {
-    "bls12_381": (P, 14, "bls12_381_consts.hpp"),
-    "bn254": (0x30644E72E131A029B85045B68181585D97816A916871CA8D3C208C16D87CFD47, 10, "bn254_consts.hpp"),
+FIELDS = {  # p, limbs, limb bits, constants header
+    "bls12_381": (P, 14, 28, "bls12_381_consts.hpp"),
+    "bn254": (0x30644E72E131A029B85045B68181585D97816A916871CA8D3C208C16D87CFD47, 9, 29, "bn254_consts.hpp"),
 }
 
 
 def use_field(name):
     """Re-point the model at another field (the device code is generic over the traits struct)."""
-    global P, NL, R, P_L, P_OVER_R, P_TOP, C
-    P, NL, hdr = FIELDS[name]
+    global P, NL, LB, LM, R, P_L, P_OVER_R, P_TOP, C
+    P, NL, LB, hdr = FIELDS[name]
+    LM = (1 << LB) - 1
     R = 1 << (LB * NL)
     P_L = [(P >> (LB * i)) & LM for i in range(NL)]
     P_OVER_R = P / R * UP

@@ -34,11 +34,12 @@ KB = [(2, 28), (4, 28), (8, 28), (8, 29), (16, 28), (32, 28), (32, 29), (64, 28)
 # BN254 base field (config 5; ark-bn254 0.2 Fq): 10 x 28-bit limbs, R = 2^280
 BN_P = 0x30644E72E131A029B85045B68181585D97816A916871CA8D3C208C16D87CFD47
 BN_R = 0x30644E72E131A029B85045B68181585D2833E84879B9709143E1F593F0000001
-BN_NL = 10
+BN_NL = 9   # 9 x 29-bit limbs (261 bits for a 254-bit p): 81 products per multiply, not 100
+BN_LB = 29
 
 
-def limbs28(x, n=NL):
-    return [(x >> (LB * i)) & ((1 << LB) - 1) for i in range(n)]
+def limbs28(x, n=NL, lb=LB):
+    return [(x >> (lb * i)) & ((1 << lb) - 1) for i in range(n)]
 
 
 def words32(x, n=12):
@@ -54,23 +55,23 @@ def mont(x):
     return x * RM % P
 
 
-def borrowed(c, L, p=None, nl=NL, vmax=None):
+def borrowed(c, L, p=None, nl=NL, vmax=None, lb=LB):
     """c p in the borrowed limb form; its top limb must dominate the top limb of any normalized
     subtrahend of value < vmax p (default c - 0.001)."""
     p = P if p is None else p
     vmax = c - 0.001 if vmax is None else vmax
-    k = limbs28(c * p, nl)
-    assert sum(v << (LB * i) for i, v in enumerate(k)) == c * p
-    hi, lo = 1 << L, 1 << (L - LB)
+    k = limbs28(c * p, nl, lb)
+    assert sum(v << (lb * i) for i, v in enumerate(k)) == c * p
+    hi, lo = 1 << L, 1 << (L - lb)
     out = list(k)
     out[0] += hi
     for i in range(1, nl - 1):
         out[i] += hi - lo
     out[nl - 1] -= lo
-    assert sum(v << (LB * i) for i, v in enumerate(out)) == c * p
+    assert sum(v << (lb * i) for i, v in enumerate(out)) == c * p
     assert all(0 <= v < (1 << 32) for v in out)
     assert min(out[: nl - 1]) >= hi - lo
-    assert out[nl - 1] >= int(vmax * 1000) * p // 1000 >> (LB * (nl - 1)), (c, L)
+    assert out[nl - 1] >= int(vmax * 1000) * p // 1000 >> (lb * (nl - 1)), (c, L)
     return out
 
 
@@ -111,30 +112,34 @@ def sliding_window(e, w):
     return steps
 
 
-def field_struct(name, p, nl, nw, kb, comment):
-    """Field parameters as a traits struct consumed by the generic field core (csrc/fp381.hpp)."""
-    rm = 1 << (LB * nl)
-    assert p % 4 == 3 and p < rm // 2048
-    pinv = (-pow(p, -1, 1 << LB)) % (1 << LB)
+def field_struct(name, p, nl, nw, kb, comment, lb=LB, headroom=2048):
+    """Field parameters as a traits struct consumed by the generic field core (csrc/fp381.hpp).
+    lb = limb bits; headroom = the value bound (in units of p) that must fit below R."""
+    rm = 1 << (lb * nl)
+    assert p % 4 == 3 and p < rm // headroom
+    pinv = (-pow(p, -1, 1 << lb)) % (1 << lb)
+    L28 = lambda x: limbs28(x, nl, lb)  # noqa: E731
     steps = sliding_window((p - 3) // 4, W)
     nmul = sum(1 for st in steps if st[1] >= 0) - 1
     nsq = sum(st[0] for st in steps)
-    L = [f"// {comment}: {nl} x {LB}-bit limbs, Montgomery R = 2^{LB * nl}.",
+    L = [f"// {comment}: {nl} x {lb}-bit limbs, Montgomery R = 2^{lb * nl}.",
          f"struct {name} {{",
          f"  static constexpr int NL = {nl};  // limbs",
+         f"  static constexpr int LB = {lb};  // bits per limb (each held in a 32-bit register)",
+         f"  static constexpr uint32_t MASK = 0x{(1 << lb) - 1:08x}u;",
          f"  static constexpr int NW = {nw};  // 32-bit words of a serialized coordinate",
-         "  " + arr("P", limbs28(p, nl)),
-         f"  static constexpr uint32_t PINV = 0x{pinv:07x}u;  // -p^-1 mod 2^28",
-         "  " + arr("R2", limbs28(rm * rm % p, nl), "R^2 mod p"),
-         "  " + arr("ONE", limbs28(rm % p, nl), "R mod p (Montgomery 1)"),
-         f"  static constexpr double INV_RHO = {float((1 << (LB * (nl - 1))) / p)!r};  "
-         f"// 2^{LB * (nl - 1)} / p (fp_is_zero quotient estimate)"]
+         "  " + arr("P", L28(p)),
+         f"  static constexpr uint32_t PINV = 0x{pinv:08x}u;  // -p^-1 mod 2^{lb}",
+         "  " + arr("R2", L28(rm * rm % p), "R^2 mod p"),
+         "  " + arr("ONE", L28(rm % p), "R mod p (Montgomery 1)"),
+         f"  static constexpr double INV_RHO = {float((1 << (lb * (nl - 1))) / p)!r};  "
+         f"// 2^{lb * (nl - 1)} / p (fp_is_zero quotient estimate)"]
     for c in (1, 2, 4, 8, 16, 32, 64, 128):
-        L.append("  " + arr(f"P_X{c}", limbs28(c * p, nl), f"{c} p, normalized (canonical reduction)"))
+        L.append("  " + arr(f"P_X{c}", L28(c * p), f"{c} p, normalized (canonical reduction)"))
     for c, Lb, vmax, alias in kb:
         nm = alias or f"KB_{c}_{Lb}"
-        L.append("  " + arr(nm, borrowed(c, Lb, p, nl, vmax),
-                            f"{c} p, limbs >= 2^{Lb} - 2^{Lb - LB}, dominates values < {vmax if vmax else c - 0.001} p"))
+        L.append("  " + arr(nm, borrowed(c, Lb, p, nl, vmax, lb),
+                            f"{c} p, limbs >= 2^{Lb} - 2^{Lb - lb}, dominates values < {vmax if vmax else c - 0.001} p"))
     L += ["  " + arr("P_WORDS", words32(p, nw), f"p as {nw} x 32-bit words (byte-level range checks)"),
           f"  // a^((p-3)/4): sliding window w={W}, table a, a^3, .., a^{2 ** W - 1}; {nsq} squarings + {nmul} "
           f"multiplications after the table ({2 ** (W - 1)} entries).",
@@ -209,8 +214,9 @@ def main():
 
     # BN254 (config 5): only the decompress chain runs here; fp_eq compares against normalized
     # values < 4p, which KB_8_28 dominates even with the small top limb of a 254-bit p
-    bn_rm = 1 << (LB * BN_NL)
-    fs, nsq, nmul = field_struct("Bn254Fp", BN_P, BN_NL, 8, [(8, 28, 4, "KB_EQ")], "BN254 Fq (ark-bn254 0.2)")
+    bn_rm = 1 << (BN_LB * BN_NL)
+    fs, nsq, nmul = field_struct("Bn254Fp", BN_P, BN_NL, 8, [(8, 29, 4, "KB_EQ")], "BN254 Fq (ark-bn254 0.2)",
+                                 lb=BN_LB, headroom=64)
     lines = [
         "// GENERATED by tools/gen_constants.py — do not edit by hand.",
         "#pragma once",
@@ -218,8 +224,9 @@ def main():
         "namespace kzgpot {",
     ] + fs + [
         "// BN254 G1: y^2 = x^3 + 3, cofactor 1",
-        arr("BN_THREE", limbs28(3 * bn_rm % BN_P, BN_NL), "3 R mod p"),
-        arr("BN_ARK_R", limbs28((1 << 256) * bn_rm % BN_P, BN_NL), "2^256 R mod p (ark-ff Fp256 Montgomery form)"),
+        arr("BN_THREE", limbs28(3 * bn_rm % BN_P, BN_NL, BN_LB), "3 R mod p"),
+        arr("BN_ARK_R", limbs28((1 << 256) * bn_rm % BN_P, BN_NL, BN_LB),
+            "2^256 R mod p (ark-ff Fp256 Montgomery form)"),
         arr("BN_FR_R", words32(BN_R, 8), "group order r"),
         "}  // namespace kzgpot",
         "",
