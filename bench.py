@@ -54,6 +54,12 @@ def parse():
     ap.add_argument("--seed", type=int, default=0x5EED)
     ap.add_argument("--no-gather", action="store_true", help="skip the RCCL all-gather (N > 1)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL, the product path) or gloo (rehearsal)")
+    ap.add_argument("--gather-impl", default="lib", choices=("lib", "torch"),
+                    help="N > 1 with nccl: lib = the library's decode + RCCL all-gather (kzgpot_decode_allgather_dev, "
+                         "the product path); torch = torch.distributed all_gather_into_tensor around _dev launches")
+    ap.add_argument("--gather-at-1", action="store_true",
+                    help="run the N > 1 sharded + gathered path with one rank (rehearses the library's RCCL path "
+                         "on a one-GPU box; the number is not the N = 1 headline)")
     ap.add_argument("--gather-chunks", type=int, default=8,
                     help="N > 1: chunks per rank; each chunk's all-gather overlaps the next chunk's decode")
     ap.add_argument("--no-verify", action="store_true")
@@ -153,7 +159,7 @@ class Sharded:
     (kzgpot/dist.py) in `chunks` chunks whose in-place all-gathers overlap the next chunk's
     decoding, into one contiguous arkworks buffer on every rank; otherwise one contiguous shard."""
 
-    def __init__(self, kind, n, seed, chunks, rank, world, gather, dev, verify):
+    def __init__(self, kind, n, seed, chunks, rank, world, gather, dev, verify, comm=None):
         import torch
 
         from kzgpot import device as D
@@ -162,7 +168,10 @@ class Sharded:
         self.D, self.KD, self.torch = D, KD, torch
         self.kind, self.n, self.seed, self.rank, self.world, self.gather = kind, n, seed, rank, world, gather
         self.rin, self.rout, self.op = RECORDS[kind]
-        if gather:
+        self.comm, self.chunks = (comm if gather else None), chunks
+        if self.comm is not None:  # the library's own decode + RCCL all-gather (kzgpot_decode_allgather_dev)
+            self.blocks = KD.lib_local_ranges(n, rank, world, chunks)
+        elif gather:
             b = KD.cyclic_block(n, world, chunks)
             self.blocks = [(g, b) for g in KD.owned_block_starts(n, rank, world, chunks)]
         else:
@@ -194,6 +203,16 @@ class Sharded:
 
     def step(self, marks):
         """Launch every block; returns the collective handles (wait on them before reading out)."""
+        if self.comm is not None:  # one library call: decode + pipelined in-place RCCL all-gathers
+            e = None
+            if marks is not None:
+                e = [self.torch.cuda.Event(enable_timing=True) for _ in range(2)]
+                e[0].record()
+            self.comm.decode_allgather(self.op, self.comp, self.n, self.chunks, self.out, self.keys[0:1])
+            if marks is not None:
+                e[1].record()
+                marks.append((self.kind, e))
+            return []
         if self.gather:
             return self.KD.decode_gather_pipelined(lambda c, g0, dst: self.launch(c, marks), self.out, self.rout,
                                                    self.n, self.rank, self.world, len(self.blocks))
@@ -202,6 +221,8 @@ class Sharded:
         return []
 
     def bad_key(self):
+        if self.comm is not None:  # already global (all-reduced inside the library)
+            return self.D.read_key(self.keys[0:1])
         return min(self.KD.key_with_offset(self.D.read_key(self.keys[c:c + 1]), self.blocks[c][0])
                    for c in range(len(self.blocks)))
 
@@ -214,14 +235,16 @@ class Sharded:
             ok = ok and torch.equal(self.dst(c), e)
         if self.gather and self.world > 1:
             b = self.blocks[0][1]
-            nb = self.out.numel() // (b * self.rout)
+            nb = self.world * self.chunks  # the exchanged blocks (a library-layout tail is every rank's own)
             mine = torch.zeros(nb, 2, dtype=torch.int64, device=self.out.device)
             w = torch.arange(1, b * self.rout // 8 + 1, dtype=torch.int64, device=self.out.device)
             for (g0, cnt), e in zip(self.blocks, self.exps):
+                if cnt != b or g0 >= nb * b:
+                    continue
                 v = e.view(torch.int64)
                 mine[g0 // cnt] = torch.stack([v.sum(), (v * w).sum()])
             dist.all_reduce(mine)  # each block has exactly one owner
-            got = self.out.view(torch.int64).view(nb, -1)
+            got = self.out[:nb * b * self.rout].view(torch.int64).view(nb, -1)
             ok = ok and torch.equal(torch.stack([got.sum(1), (got * w).sum(1)], 1), mine)
         self.exps = None
         return bool(ok)
@@ -395,6 +418,11 @@ def e2e_preprocess(n_log2, seed, dev, kzgpot, D):
 
 def main():
     args = parse()
+    # The one JSON line goes to the real stdout; anything native libraries print there (RCCL's
+    # version banner at communicator init) is sent to stderr instead.
+    sys.stdout.flush()
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -419,11 +447,21 @@ def main():
     from kzgpot import dist as KD
 
     n1, n2 = 1 << args.g1_log2, 1 << args.g2_log2
-    gather = world > 1 and not args.no_gather
+    gather = (world > 1 or args.gather_at_1) and not args.no_gather
     verify = not args.no_verify
     t_gen = time.perf_counter()
-    g1 = Sharded("g1", n1, args.seed, args.gather_chunks, rank, world, gather, dev, verify)
-    g2 = Sharded("g2", n2, args.seed + 1, 1, rank, world, gather, dev, verify)  # 2^16 points: one chunk
+    comm, gather_impl = None, None
+    if gather:
+        gather_impl = "torch.distributed"
+        if args.gather_impl == "lib" and args.dist_backend == "nccl":
+            try:
+                comm = KD.LibComm(rank, world)
+                gather_impl = "libkzgpot (kzgpot_decode_allgather_dev: RCCL inside the library)"
+            except (OSError, RuntimeError) as e:  # reported in the line; the torch path is the same layout
+                print(f"warning: library communicator unavailable ({e}); torch.distributed gathers", file=sys.stderr)
+                gather_impl = f"torch.distributed (library communicator failed: {e})"
+    g1 = Sharded("g1", n1, args.seed, args.gather_chunks, rank, world, gather, dev, verify, comm)
+    g2 = Sharded("g2", n2, args.seed + 1, 1, rank, world, gather, dev, verify, comm)  # 2^16 points: one chunk
     torch.cuda.synchronize()
     t_gen = time.perf_counter() - t_gen
 
@@ -441,7 +479,7 @@ def main():
         del g1.comp
         nb = 1 << args.bn254_log2
         t_bn = time.perf_counter()
-        bn = Sharded("bn254", nb, args.seed + 2, args.gather_chunks, rank, world, gather, dev, verify)
+        bn = Sharded("bn254", nb, args.seed + 2, args.gather_chunks, rank, world, gather, dev, verify, comm)
         torch.cuda.synchronize()
         t_bn = time.perf_counter() - t_bn
         bn_s, bn_ev, bn_ok = timed([bn], args.steps, 1, world, dev, verify)
@@ -560,7 +598,7 @@ def main():
                             "points -> arkworks uncompressed, subgroup-checked"
                             + (f", block-cyclic shards, RCCL all-gather to one contiguous buffer pipelined in "
                                f"{args.gather_chunks} chunks" if gather else ""),
-                "g1_points": n1, "g2_points": n2, "parallelism": f"shard{world}",
+                "g1_points": n1, "g2_points": n2, "parallelism": f"shard{world}", "gather_impl": gather_impl,
                 "subgroup_test": "endomorphism (phi/psi), bit-exact accept/reject vs ark mul_bits(r)",
             },
             "roofline": {
@@ -589,9 +627,11 @@ def main():
                                                   D.synth("g1", args.seed, 0, 1 << args.cpu_sample_log2, dev,
                                                           with_expected=False)[0],
                                                   g2.comp, args.cpu_sample_log2)
-        print(json.dumps(result), flush=True)
+        print(json.dumps(result), file=json_out, flush=True)
     if world > 1:
         dist.barrier()
+        if comm is not None:
+            comm.close()
         dist.destroy_process_group()
     return result
 

@@ -190,6 +190,38 @@ int kzgpot_bn254_g1_decompress_ex(const uint8_t* in, size_t n, uint8_t* out, int
 int kzgpot_bn254_g1_decompress_dev(const void* d_in, size_t n, void* d_out, uint64_t* d_bad_key, uint8_t* d_status,
                                    void* stream);
 
+/* ---------------------------------------------------------------- multi-GPU, RCCL inside */
+/* north_star: "the τ^i array shards trivially across the 8 GPUs of one node with a final RCCL
+ * all-gather over xGMI to produce one contiguous arkworks buffer". Replaces the reference's only
+ * parallel stage, the chunked decompression of powersoftau's Accumulator::deserialize
+ * (src/bin/preprocess-kgz.rs:105-110), whose workers fill disjoint slices of one Vec — here the
+ * slices live on different GPUs and RCCL assembles them. One process (or thread) per GPU.
+ *   rank 0: kzgpot_comm_unique_id(id); ship the 128 bytes to every rank (MPI, torch.distributed,
+ *   a file, ...); every rank, with its GPU current: kzgpot_comm_init(&comm, id, nranks, rank). */
+#define KZGPOT_COMM_ID_BYTES 128
+int kzgpot_comm_unique_id(uint8_t* id);
+int kzgpot_comm_init(void** comm, const uint8_t* id, int nranks, int rank); /* collective */
+int kzgpot_comm_destroy(void* comm);
+#define KZGPOT_OP_G1_DECOMPRESS 0
+#define KZGPOT_OP_G2_DECOMPRESS 1
+#define KZGPOT_OP_G1_TRANSCODE 2
+#define KZGPOT_OP_G2_TRANSCODE 3
+#define KZGPOT_OP_BN254_G1_DECOMPRESS 4
+/* Block-cyclic layout of n points over nranks x chunks: *block = floor(n / (nranks chunks)) points
+ * per block, *tail = the n - nranks chunks block points at the end. Rank k owns blocks
+ * c nranks + k (global points [(c nranks + k) block, +block)), c = 0..chunks-1; every rank also
+ * decodes the tail. */
+int kzgpot_shard_layout(uint64_t n, int nranks, uint32_t chunks, uint64_t* block, uint64_t* tail);
+/* Collective, asynchronous on `stream` (a hipStream_t of the communicator's GPU). d_in_local =
+ * this rank's input records: its `chunks` owned blocks in chunk order, then the tail (chunks x
+ * block + tail records). d_out = all n output records (HBM, every rank). Each chunk is decoded
+ * on `stream` and then all-gathered in place (ncclAllGather on the communicator's own stream)
+ * while the next chunk decodes. *d_bad_key = the first rejected point over ALL ranks as
+ * (global index << 8) | status, or all ones (decode with kzgpot_decode_bad_key); rejected
+ * records are zero-filled as in the single-GPU calls. `stream` waits for the gathers. */
+int kzgpot_decode_allgather_dev(void* comm, int op, const void* d_in_local, uint64_t n, uint32_t chunks, void* d_out,
+                                uint32_t flags, uint64_t* d_bad_key, void* stream);
+
 /* ---------------------------------------------------------------- misc */
 const char* kzgpot_status_name(int status);  /* name of a KZGPOT_ST_* or KZGPOT_E_* code */
 int kzgpot_device_count(void);               /* visible HIP devices (0 if none) */

@@ -1,0 +1,251 @@
+// Multi-GPU path inside the library (north_star "the τ^i array shards trivially across
+// the 8 GPUs of one node with a final RCCL all-gather over xGMI to produce one contiguous arkworks
+// buffer"): one process (or thread) per GPU, each holding a kzgpot communicator (an RCCL comm plus
+// a private comm stream), and one call that decodes the rank's share of a point stream and
+// assembles the whole arkworks buffer in HBM on every rank.
+//
+// The reference has no parallel exchange at all: its only parallel stage is the chunked
+// decompression inside powersoftau's Accumulator::deserialize (src/bin/preprocess-kgz.rs:105-110),
+// whose workers write disjoint slices of one Vec. Here the slices are block-cyclic over the ranks
+// so that the exchange can be pipelined behind the decoding:
+//
+//   n points = nranks x chunks blocks of B = floor(n / (nranks chunks)) points + a tail of
+//   r = n - nranks chunks B points (r < nranks chunks, e.g. τG1's 2^22 - 1 points);
+//   rank k owns blocks c nranks + k (c < chunks); chunk c's nranks blocks are adjacent in the
+//   output, so after the rank's chunk-c decode ONE in-place ncclAllGather fills that contiguous
+//   region, on the comm stream, while the caller's stream decodes chunk c + 1. Only the last
+//   chunk's gather is exposed. The tail is decoded by every rank (no exchange; it is < 64 points
+//   in any layout a caller would pick).
+//
+// The first rejected point over all ranks is one 8-byte ncclAllReduce(min) of the per-launch keys
+// shifted to global indices (k_merge_keys), so every rank returns the same deterministic answer.
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <mutex>
+#include <vector>
+
+#include "codec.hpp"
+
+using namespace kzgpot;
+
+namespace {
+
+// RCCL is bound at first use, not at link time: a process that already holds an RCCL (torch does:
+// its own librccl.so with the same SONAME) must keep using that one — a second copy loaded ahead
+// of torch corrupts the heap at exit — and single-GPU users never load it at all.
+struct Rccl {
+  decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+  decltype(&ncclCommInitRank) comm_init_rank = nullptr;
+  decltype(&ncclCommDestroy) comm_destroy = nullptr;
+  decltype(&ncclAllGather) all_gather = nullptr;
+  decltype(&ncclAllReduce) all_reduce = nullptr;
+  decltype(&ncclGetErrorString) error_string = nullptr;
+  bool ok = false;
+};
+const Rccl& rccl() {
+  static Rccl r;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL | RTLD_NOLOAD);  // the process's own RCCL
+    if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) {
+      fprintf(stderr, "kzgpot: cannot load librccl.so.1: %s\n", dlerror());
+      return;
+    }
+    r.get_unique_id = (decltype(r.get_unique_id))dlsym(h, "ncclGetUniqueId");
+    r.comm_init_rank = (decltype(r.comm_init_rank))dlsym(h, "ncclCommInitRank");
+    r.comm_destroy = (decltype(r.comm_destroy))dlsym(h, "ncclCommDestroy");
+    r.all_gather = (decltype(r.all_gather))dlsym(h, "ncclAllGather");
+    r.all_reduce = (decltype(r.all_reduce))dlsym(h, "ncclAllReduce");
+    r.error_string = (decltype(r.error_string))dlsym(h, "ncclGetErrorString");
+    r.ok = r.get_unique_id && r.comm_init_rank && r.comm_destroy && r.all_gather && r.all_reduce && r.error_string;
+  });
+  return r;
+}
+
+#define HIP_OK(expr)                                                                                        \
+  do {                                                                                                      \
+    hipError_t e_ = (expr);                                                                                 \
+    if (e_ != hipSuccess) {                                                                                 \
+      fprintf(stderr, "kzgpot: %s failed: %s (%s:%d)\n", #expr, hipGetErrorString(e_), __FILE__, __LINE__); \
+      return KZGPOT_E_DEVICE;                                                                               \
+    }                                                                                                       \
+  } while (0)
+#define NCCL_OK(expr)                                                                                          \
+  do {                                                                                                         \
+    ncclResult_t e_ = (expr);                                                                                  \
+    if (e_ != ncclSuccess) {                                                                                   \
+      fprintf(stderr, "kzgpot: %s failed: %s (%s:%d)\n", #expr, rccl().error_string(e_), __FILE__, __LINE__); \
+      return KZGPOT_E_DEVICE;                                                                                  \
+    }                                                                                                          \
+  } while (0)
+
+struct Comm {
+  ncclComm_t nccl = nullptr;
+  int rank = 0, nranks = 1, device = -1;
+  hipStream_t cs = nullptr;               // the comm stream: gathers + the key all-reduce
+  std::vector<hipEvent_t> ev;             // one per chunk (decode done) + 1 (keys merged) + 1 (all done)
+  unsigned long long* d_keys = nullptr;   // per-launch keys (chunks + tail)
+  uint64_t* d_local = nullptr;            // this rank's global-index min key
+  size_t cap_keys = 0;
+  std::mutex mu;                          // one call at a time per communicator (events are reused)
+};
+
+bool op_from_code(int code, CodecOp* op) {
+  switch (code) {
+    case KZGPOT_OP_G1_DECOMPRESS: *op = CodecOp::G1Decompress; return true;
+    case KZGPOT_OP_G2_DECOMPRESS: *op = CodecOp::G2Decompress; return true;
+    case KZGPOT_OP_G1_TRANSCODE: *op = CodecOp::G1Transcode; return true;
+    case KZGPOT_OP_G2_TRANSCODE: *op = CodecOp::G2Transcode; return true;
+    case KZGPOT_OP_BN254_G1_DECOMPRESS: *op = CodecOp::Bn254G1Decompress; return true;
+    default: return false;
+  }
+}
+
+// keys[j] (j < chunks: block j nranks + rank, j == chunks: the tail) hold (local index << 8) |
+// status or all ones; out = min over j of the key shifted to the global index.
+__global__ void k_merge_keys(const unsigned long long* __restrict__ keys, uint32_t chunks, uint64_t block,
+                             uint32_t nranks, uint32_t rank, uint64_t* __restrict__ out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  uint64_t best = ~0ull;
+  for (uint32_t j = 0; j <= chunks; j++) {
+    const uint64_t k = keys[j];
+    if (k == ~0ull) continue;
+    const uint64_t base = j < chunks ? ((uint64_t)j * nranks + rank) * block : (uint64_t)chunks * nranks * block;
+    const uint64_t g = (((k >> 8) + base) << 8) | (k & 0xff);
+    best = g < best ? g : best;
+  }
+  out[0] = best;
+}
+
+int ensure_events(Comm& c, size_t need) {
+  while (c.ev.size() < need) {
+    hipEvent_t e;
+    HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    c.ev.push_back(e);
+  }
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int kzgpot_comm_unique_id(uint8_t* id) {
+  if (!id) return KZGPOT_E_INVALID_ARG;
+  static_assert(sizeof(ncclUniqueId) == KZGPOT_COMM_ID_BYTES, "RCCL unique id size");
+  if (!rccl().ok) return KZGPOT_E_DEVICE;
+  ncclUniqueId u;
+  NCCL_OK(rccl().get_unique_id(&u));
+  memcpy(id, &u, sizeof u);
+  return 0;
+}
+
+int kzgpot_comm_init(void** comm, const uint8_t* id, int nranks, int rank) {
+  if (!comm || !id || nranks < 1 || rank < 0 || rank >= nranks) return KZGPOT_E_INVALID_ARG;
+  *comm = nullptr;
+  if (!rccl().ok) return KZGPOT_E_DEVICE;
+  int dev = -1;
+  HIP_OK(hipGetDevice(&dev));
+  Comm* c = new Comm;
+  c->rank = rank;
+  c->nranks = nranks;
+  c->device = dev;
+  ncclUniqueId u;
+  memcpy(&u, id, sizeof u);
+  const ncclResult_t r = rccl().comm_init_rank(&c->nccl, nranks, u, rank);
+  if (r != ncclSuccess) {
+    fprintf(stderr, "kzgpot: ncclCommInitRank(%d of %d) failed: %s\n", rank, nranks, rccl().error_string(r));
+    delete c;
+    return KZGPOT_E_DEVICE;
+  }
+  if (hipStreamCreateWithFlags(&c->cs, hipStreamNonBlocking) != hipSuccess ||
+      hipMalloc(&c->d_local, sizeof(uint64_t)) != hipSuccess) {
+    rccl().comm_destroy(c->nccl);
+    delete c;
+    return KZGPOT_E_DEVICE;
+  }
+  *comm = c;
+  return 0;
+}
+
+int kzgpot_comm_destroy(void* comm) {
+  if (!comm) return KZGPOT_E_INVALID_ARG;
+  Comm* c = (Comm*)comm;
+  int prev = -1;
+  (void)hipGetDevice(&prev);
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->cs);
+  for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
+  if (c->d_keys) (void)hipFree(c->d_keys);
+  if (c->d_local) (void)hipFree(c->d_local);
+  (void)hipStreamDestroy(c->cs);
+  const ncclResult_t r = rccl().comm_destroy(c->nccl);
+  if (prev >= 0) (void)hipSetDevice(prev);
+  delete c;
+  return r == ncclSuccess ? 0 : KZGPOT_E_DEVICE;
+}
+
+int kzgpot_shard_layout(uint64_t n, int nranks, uint32_t chunks, uint64_t* block, uint64_t* tail) {
+  if (nranks < 1 || chunks < 1 || !block || !tail) return KZGPOT_E_INVALID_ARG;
+  *block = n / ((uint64_t)nranks * chunks);
+  *tail = n - *block * (uint64_t)nranks * chunks;
+  return 0;
+}
+
+int kzgpot_decode_allgather_dev(void* comm, int op_code, const void* d_in_local, uint64_t n, uint32_t chunks,
+                                void* d_out, uint32_t flags, uint64_t* d_bad_key, void* stream) {
+  CodecOp op;
+  if (!comm || !op_from_code(op_code, &op) || chunks < 1 || !d_bad_key || (n && (!d_in_local || !d_out)))
+    return KZGPOT_E_INVALID_ARG;
+  Comm& c = *(Comm*)comm;
+  std::lock_guard<std::mutex> lock(c.mu);
+  int dev = -1;
+  HIP_OK(hipGetDevice(&dev));
+  if (dev != c.device) return KZGPOT_E_INVALID_ARG;  // the communicator's GPU must be current
+  if (op == CodecOp::Bn254G1Decompress || op == CodecOp::G1Transcode || op == CodecOp::G2Transcode)
+    flags &= KZGPOT_SUBGROUP_REF;
+  hipStream_t s = (hipStream_t)stream;
+  const uint64_t rin = in_record(op), rout = out_record(op);
+  uint64_t B = 0, tail = 0;
+  kzgpot_shard_layout(n, c.nranks, chunks, &B, &tail);
+  if (c.cap_keys < chunks + 1) {
+    if (c.d_keys) HIP_OK(hipFree(c.d_keys));
+    c.d_keys = nullptr;
+    c.cap_keys = 0;
+    HIP_OK(hipMalloc(&c.d_keys, (chunks + 1) * sizeof(unsigned long long)));
+    c.cap_keys = chunks + 1;
+  }
+  if (ensure_events(c, chunks + 2)) return KZGPOT_E_DEVICE;
+  HIP_OK(hipMemsetAsync(c.d_keys, 0xff, (chunks + 1) * sizeof(unsigned long long), s));
+  const uint8_t* in = (const uint8_t*)d_in_local;
+  uint8_t* out = (uint8_t*)d_out;
+  const size_t bytes = (size_t)(B * rout);
+  for (uint32_t ch = 0; B && ch < chunks; ch++) {
+    const uint64_t g0 = ((uint64_t)ch * c.nranks + c.rank) * B;
+    HIP_OK(launch_codec(op, in + ch * B * rin, out + g0 * rout, B, flags, c.d_keys + ch, nullptr, s));
+    HIP_OK(hipEventRecord(c.ev[ch], s));
+    HIP_OK(hipStreamWaitEvent(c.cs, c.ev[ch], 0));
+    uint8_t* region = out + (uint64_t)ch * c.nranks * B * rout;
+    NCCL_OK(rccl().all_gather(region + (size_t)c.rank * bytes, region, bytes, ncclUint8, c.nccl, c.cs));
+  }
+  if (tail)
+    HIP_OK(launch_codec(op, in + (uint64_t)chunks * B * rin, out + (uint64_t)chunks * c.nranks * B * rout, tail,
+                        flags, c.d_keys + chunks, nullptr, s));
+  hipLaunchKernelGGL(k_merge_keys, dim3(1), dim3(64), 0, s, c.d_keys, chunks, B, (uint32_t)c.nranks,
+                     (uint32_t)c.rank, c.d_local);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipEventRecord(c.ev[chunks], s));
+  HIP_OK(hipStreamWaitEvent(c.cs, c.ev[chunks], 0));
+  NCCL_OK(rccl().all_reduce(c.d_local, d_bad_key, 1, ncclUint64, ncclMin, c.nccl, c.cs));
+  HIP_OK(hipEventRecord(c.ev[chunks + 1], c.cs));
+  HIP_OK(hipStreamWaitEvent(s, c.ev[chunks + 1], 0));  // the caller's stream sees the whole buffer
+  return 0;
+}
+
+}  // extern "C"

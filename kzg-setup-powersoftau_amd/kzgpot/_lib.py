@@ -57,6 +57,11 @@ SIGNATURES = {
     "kzgpot_bn254_g1_decompress": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, i64p]),
     "kzgpot_bn254_g1_decompress_ex": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, i64p, ctypes.c_void_p]),
     "kzgpot_bn254_g1_decompress_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "kzgpot_comm_unique_id": (ctypes.c_int, [ctypes.c_void_p]),
+    "kzgpot_comm_init": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
+    "kzgpot_comm_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "kzgpot_shard_layout": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_int, ctypes.c_uint32, u64p, u64p]),
+    "kzgpot_decode_allgather_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]),
     "kzgpot_status_name": (ctypes.c_char_p, [ctypes.c_int]),
     "kzgpot_device_count": (ctypes.c_int, []),
     "kzgpot_version": (ctypes.c_char_p, []),

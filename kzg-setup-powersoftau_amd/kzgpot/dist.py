@@ -79,6 +79,74 @@ def decode_gather_pipelined(decode, full: torch.Tensor, rec_out: int, n: int, ra
     return works
 
 
+def shard_layout(n: int, world: int, chunks: int) -> tuple[int, int]:
+    """(block, tail) of the library's block-cyclic layout (kzgpot_shard_layout, include/kzgpot.h):
+    world x chunks blocks of floor(n / (world chunks)) points, then a tail every rank decodes."""
+    b = n // (world * chunks)
+    return b, n - b * world * chunks
+
+
+def lib_local_ranges(n: int, rank: int, world: int, chunks: int) -> list[tuple[int, int]]:
+    """Global (first point, count) ranges whose inputs rank's d_in_local holds, in order: its
+    owned blocks c world + rank, then the tail."""
+    b, tail = shard_layout(n, world, chunks)
+    rng = [((c * world + rank) * b, b) for c in range(chunks)] if b else []
+    if tail:
+        rng.append((b * world * chunks, tail))
+    return rng
+
+
+LIB_OPS = {"g1_decompress": 0, "g2_decompress": 1, "g1_transcode": 2, "g2_transcode": 3, "bn254_g1_decompress": 4}
+
+
+class LibComm:
+    """A kzgpot communicator: RCCL inside libkzgpot.so (kzgpot_comm_init), so the decode and the
+    all-gather that assembles the contiguous arkworks buffer are one library call
+    (kzgpot_decode_allgather_dev). The 128-byte RCCL id travels over torch.distributed."""
+
+    def __init__(self, rank: int, world: int, group=None):
+        import ctypes
+
+        from . import _lib
+
+        self._ct, self.lib = ctypes, _lib.load()
+        self.rank, self.world = rank, world
+        uid = ctypes.create_string_buffer(128)
+        if rank == 0:
+            rc = self.lib.kzgpot_comm_unique_id(uid)
+            if rc:
+                raise RuntimeError(f"kzgpot_comm_unique_id failed ({rc})")
+        if world > 1:
+            obj = [uid.raw]
+            dist.broadcast_object_list(obj, src=0, group=group)
+            uid = ctypes.create_string_buffer(obj[0], 128)
+        self.handle = ctypes.c_void_p()
+        rc = self.lib.kzgpot_comm_init(ctypes.byref(self.handle), uid, world, rank)
+        if rc:
+            raise RuntimeError(f"kzgpot_comm_init({rank} of {world}) failed ({rc})")
+
+    def decode_allgather(self, op: str, d_in_local: torch.Tensor, n: int, chunks: int, d_out: torch.Tensor,
+                         key: torch.Tensor, flags: int = 0) -> None:
+        """Asynchronous on torch's current stream: this rank's blocks decoded, every block
+        all-gathered into d_out (n records on every rank), key = global first bad point."""
+        from .device import _DEV_FNS
+
+        _, rin, rout = _DEV_FNS[op]
+        need_in = sum(c for _, c in lib_local_ranges(n, self.rank, self.world, chunks)) * rin
+        if d_in_local.numel() < need_in or d_out.numel() < n * rout:
+            raise ValueError(f"{op}: bad buffer sizes {d_in_local.numel()} / {d_out.numel()}")
+        rc = self.lib.kzgpot_decode_allgather_dev(self.handle, LIB_OPS[op], d_in_local.data_ptr(), n, chunks,
+                                                  d_out.data_ptr(), flags, key.data_ptr(),
+                                                  torch.cuda.current_stream().cuda_stream)
+        if rc:
+            raise RuntimeError(f"kzgpot_decode_allgather_dev({op}) failed ({rc})")
+
+    def close(self) -> None:
+        if self.handle:
+            self.lib.kzgpot_comm_destroy(self.handle)
+            self.handle = self._ct.c_void_p()
+
+
 def key_with_offset(key: int, offset: int) -> int:
     """Shift a shard-local bad key ((index << 8) | status) to global indices."""
     if key == NO_BAD:

@@ -162,3 +162,32 @@ def test_cyclic_layout():
     assert starts == list(range(0, n, b))
     with pytest.raises(ValueError):
         KD.cyclic_block(100, 8, 4)
+
+
+@pytest.mark.parametrize("n,world,chunks", [((1 << 22) - 1, 8, 8), (1 << 27, 8, 8), (100, 8, 4), (3, 2, 8), (0, 4, 2)])
+def test_library_layout_covers_every_point(kzgpot_mod, n, world, chunks):
+    """kzgpot_shard_layout (the C ABI's block-cyclic layout for kzgpot_decode_allgather_dev) and its
+    Python mirror agree; the owned blocks over all ranks plus the tail cover [0, n) exactly once,
+    and each chunk's world blocks are adjacent (one contiguous in-place all-gather per chunk)."""
+    from kzgpot import _lib
+    from kzgpot import dist as KD
+
+    blk, tl = ctypes.c_uint64(), ctypes.c_uint64()
+    assert _lib.load().kzgpot_shard_layout(n, world, chunks, ctypes.byref(blk), ctypes.byref(tl)) == 0
+    b, tail = KD.shard_layout(n, world, chunks)
+    assert (blk.value, tl.value) == (b, tail)
+    assert tail < world * chunks
+    covered = []
+    for r in range(world):
+        rng = KD.lib_local_ranges(n, r, world, chunks)
+        owned = rng[:-1] if tail else rng
+        covered += [i for g0, c in owned for i in range(g0, g0 + c)] if n < 5000 else [g0 for g0, _ in owned]
+        if tail:
+            assert rng[-1] == (n - tail, tail)  # every rank decodes the tail itself
+    if n < 5000:
+        assert sorted(covered) == list(range(n - tail))
+    else:
+        assert sorted(covered) == list(range(0, n - tail, b))
+    for c in range(chunks):  # chunk c = blocks c*world .. c*world + world - 1, contiguous
+        starts = sorted(KD.lib_local_ranges(n, r, world, chunks)[c][0] for r in range(world)) if b else []
+        assert starts == [(c * world + r) * b for r in range(world)] if b else True
