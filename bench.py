@@ -37,7 +37,8 @@ HBM_PEAK_GBS = 8000.0           # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 SIMDS, CLOCK_HZ = 256 * 4, 2.4e9  # MI355X: 256 CUs x 4 SIMDs at the 2.4 GHz peak engine clock
 ALG_BYTES = {"g1": 144, "g2": 288, "bn254": 96}  # bytes read + written per point
 # kernel -> its name in profiles/r02_valu_mix.json (demangled; the check kernels' Src 0 = ArkInPlace)
-MIX_NAMES = {"k_g1_decompress": "kzgpot::k_g1_decompress(", "k_g1_check": "kzgpot::k_g1_check<(kzgpot::Src)0>",
+MIX_NAMES = {"k_g1_codec": "kzgpot::k_g1_codec(",
+             "k_g1_decompress": "kzgpot::k_g1_decompress(", "k_g1_check": "kzgpot::k_g1_check<(kzgpot::Src)0>",
              "k_g2_decompress": "kzgpot::k_g2_decompress(", "k_g2_check": "kzgpot::k_g2_check<(kzgpot::Src)0>",
              "k_bn254_g1_decompress": "kzgpot::k_bn254_g1_decompress("}
 RECORDS = {"g1": (48, 96, "g1_decompress"), "g2": (96, 192, "g2_decompress"),
@@ -62,6 +63,8 @@ def parse():
                          "on a one-GPU box; the number is not the N = 1 headline)")
     ap.add_argument("--gather-chunks", type=int, default=8,
                     help="N > 1: chunks per rank; each chunk's all-gather overlaps the next chunk's decode")
+    ap.add_argument("--split-phases", action="store_true",
+                    help="G1: decompress and check as two launches (KZGPOT_SPLIT_PHASES) instead of the fused kernel")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--oracle-sample-runs", type=int, default=64,
                     help="runs of 256 output records (+ the last 256) re-decoded by the C oracle")
@@ -159,7 +162,7 @@ class Sharded:
     (kzgpot/dist.py) in `chunks` chunks whose in-place all-gathers overlap the next chunk's
     decoding, into one contiguous arkworks buffer on every rank; otherwise one contiguous shard."""
 
-    def __init__(self, kind, n, seed, chunks, rank, world, gather, dev, verify, comm=None):
+    def __init__(self, kind, n, seed, chunks, rank, world, gather, dev, verify, comm=None, flags=0):
         import torch
 
         from kzgpot import device as D
@@ -168,7 +171,7 @@ class Sharded:
         self.D, self.KD, self.torch = D, KD, torch
         self.kind, self.n, self.seed, self.rank, self.world, self.gather = kind, n, seed, rank, world, gather
         self.rin, self.rout, self.op = RECORDS[kind]
-        self.comm, self.chunks = (comm if gather else None), chunks
+        self.comm, self.chunks, self.flags = (comm if gather else None), chunks, flags
         if self.comm is not None:  # the library's own decode + RCCL all-gather (kzgpot_decode_allgather_dev)
             self.blocks = KD.lib_local_ranges(n, rank, world, chunks)
         elif gather:
@@ -196,7 +199,7 @@ class Sharded:
         if marks is not None:
             e = [self.torch.cuda.Event(enable_timing=True) for _ in range(2)]
             e[0].record()
-        self.D.codec_dev(self.op, src, self.dst(c), self.keys[c:c + 1])
+        self.D.codec_dev(self.op, src, self.dst(c), self.keys[c:c + 1], flags=self.flags)
         if marks is not None:
             e[1].record()
             marks.append((self.kind, e))
@@ -208,7 +211,7 @@ class Sharded:
             if marks is not None:
                 e = [self.torch.cuda.Event(enable_timing=True) for _ in range(2)]
                 e[0].record()
-            self.comm.decode_allgather(self.op, self.comp, self.n, self.chunks, self.out, self.keys[0:1])
+            self.comm.decode_allgather(self.op, self.comp, self.n, self.chunks, self.out, self.keys[0:1], self.flags)
             if marks is not None:
                 e[1].record()
                 marks.append((self.kind, e))
@@ -460,7 +463,9 @@ def main():
             except (OSError, RuntimeError) as e:  # reported in the line; the torch path is the same layout
                 print(f"warning: library communicator unavailable ({e}); torch.distributed gathers", file=sys.stderr)
                 gather_impl = f"torch.distributed (library communicator failed: {e})"
-    g1 = Sharded("g1", n1, args.seed, args.gather_chunks, rank, world, gather, dev, verify, comm)
+    g1_flags = 0x4 if args.split_phases else 0  # KZGPOT_SPLIT_PHASES
+    g1_kernels = ["k_g1_decompress", "k_g1_check"] if args.split_phases else ["k_g1_codec"]
+    g1 = Sharded("g1", n1, args.seed, args.gather_chunks, rank, world, gather, dev, verify, comm, g1_flags)
     g2 = Sharded("g2", n2, args.seed + 1, 1, rank, world, gather, dev, verify, comm)  # 2^16 points: one chunk
     torch.cuda.synchronize()
     t_gen = time.perf_counter() - t_gen
@@ -602,7 +607,8 @@ def main():
                 "subgroup_test": "endomorphism (phi/psi), bit-exact accept/reject vs ark mul_bits(r)",
             },
             "roofline": {
-                "kernel": "k_g1_decompress + k_g1_check<ArkInPlace> (G1 codec, one pass)",
+                "kernel": ("k_g1_decompress + k_g1_check<ArkInPlace> (G1 codec, split launches)" if args.split_phases
+                           else "k_g1_codec (G1 decompress + subgroup check + ark emit, one pass)"),
                 "bound": "hbm",
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
@@ -613,7 +619,7 @@ def main():
                 "algorithmic_bytes_per_point": ALG_BYTES["g1"],
                 "note": "integer-VALU bound, not HBM: see valu",
             },
-            "valu": valu_roofline(pmc, load_json("r02_valu_mix.json"), ["k_g1_decompress", "k_g1_check"], g1.m, g1_ms),
+            "valu": valu_roofline(pmc, load_json("r02_valu_mix.json"), g1_kernels, g1.m, g1_ms),
             "kernels_ms": {"g1_codec": g1_ms, "g2_codec": g2_ms},
             "verified_bit_exact": verified,
             "oracle_sample_check": sample,

@@ -1,4 +1,6 @@
-// The hot path: one lane per point, decompress -> check -> arkworks emit, in two kernel phases.
+// The hot path: one lane per point, decompress -> check -> arkworks emit. Checked G1 streams (the
+// headline) run both phases in ONE kernel (k_g1_codec, below); G2, unchecked G1 and the
+// KZGPOT_SPLIT_PHASES A/B mode run them as two kernels.
 //
 // Replaces, per point, the reference's three CPU passes:
 //   powersoftau Accumulator::deserialize → pairing into_affine_unchecked   (preprocess-kgz.rs:105)
@@ -16,8 +18,10 @@
 //                              pairing-uncompressed input for the read_g1/read_g2 transcode
 //                              (Src = PairingBE). Rejected records are zero-filled.
 // Splitting the phases keeps each kernel's live register set to one algorithm (the square-root
-// table or the scalar-multiplication state, not both), which is what sets occupancy here; the
-// extra traffic is one 96/192-B re-read per point, against ~1,500 Fp multiplies of work.
+// table or the scalar-multiplication state, not both); the extra traffic is one 96/192-B re-read
+// per point, against ~1,500 Fp multiplies of work. For G1 the fused kernel parks x and y in LDS
+// between the phases instead and measured the same time as the split pair on one box (2,264 vs
+// 2,265 ms per 2^27 points, VALU-bound either way) with 144 instead of 263 B/point of HBM traffic.
 //
 // HBM layout: packed records, no padding — G1 in 48 B (3 x 16-B loads per lane), out 96 B
 // (6 x 16-B stores); G2 in 96 B / out 192 B. All records are 16-B aligned.
@@ -99,6 +103,106 @@ __global__ void __launch_bounds__(kBlock) k_g1_decompress(const uint4* __restric
     store_words(dst, zx);
     store_words(dst + 3, zy);
   }
+  report(i, st, first_bad, status);
+}
+
+// ================================================================================ fused G1 codec
+// Both phases of a checked G1 point in one lane and one launch (the default for checked
+// streams): x's canonical words go out as soon as x < p is known, the Montgomery x is parked in
+// LDS before the square root, y's canonical words go out after the sign rule and its Montgomery
+// form is parked next to x — so nothing but the ladder state is live across the subgroup test,
+// and no record is read back from HBM (48 B in + 96 B out per point, against 48 + 96 + 96 + the
+// x re-read of the split kernels). A rejected point's record is zero-filled (the split path's
+// phase 2 does the same to its poison record). 70 KB of LDS per block (base point + the second
+// ladder's base, as k_g1_check) holds the kernel at 2 waves per SIMD.
+__global__ void __launch_bounds__(kBlock) k_g1_codec(const uint4* __restrict__ in, uint4* __restrict__ out,
+                                                     uint64_t n, uint32_t flags,
+                                                     unsigned long long* __restrict__ first_bad,
+                                                     uint8_t* __restrict__ status) {
+  __shared__ uint32_t base[2 * NL][kBlock];
+  __shared__ uint32_t qpark[3 * NL][kBlock];
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  int st = 0;
+  bool greatest;
+  uint4* dst = out + i * 6;
+  fp a;
+  {
+    words w;
+    load_be(w, in + i * 3);
+    const uint32_t b0 = w[11] >> 24;
+    uint32_t rest = 0;
+#pragma unroll
+    for (int k = 0; k < 11; k++) rest |= w[k];
+    const bool inf_clean = ((w[11] & 0x3fffffffu) | rest) == 0;
+    w[11] &= 0x1fffffffu;
+    if (!(b0 & 0x80u)) st = 1;
+    else if (b0 & 0x40u) st = inf_clean ? 7 : 2;  // checked stream: infinity is rejected
+    else if (words_geq_p(w)) st = 3;
+    greatest = (b0 & 0x20u) != 0;
+    if (st == 0) store_words(dst, w);  // ark x = the canonical x
+    fp t, u;
+    words_to_mont(t, w);
+#pragma unroll
+    for (int k = 0; k < NL; k++) base[k][threadIdx.x] = t.v[k];
+    fp_sqr(a, t);
+    fp_mul(a, a, t);
+    fp_set(u, FP_FOUR);
+    fp_add(a, a, u);
+  }
+  {
+    fp y, t;
+    fp_pow_pm3d4(t, a);
+    fp_mul(y, t, a);
+    fp_sqr(t, y);
+    if (st == 0 && !fp_eq(t, a)) st = 4;
+    fp yc, nyc;
+    fp_from_mont(yc, y);
+    fp_neg_canon(nyc, yc);
+    fp_select(yc, fp_lt_canon(yc, nyc) ^ greatest, yc, nyc);
+    if (st == 0) {
+      store_canon(dst + 3, yc);
+      fp_to_mont(y, yc);
+#pragma unroll
+      for (int k = 0; k < NL; k++) base[NL + k][threadIdx.x] = y.v[k];
+    }
+  }
+  if (st == 0) {
+    auto load = [&](fp& bx, fp& by) {
+      uint32_t lane = threadIdx.x;
+      asm volatile("" : "+v"(lane));  // opaque index: re-read at every use, never hoisted
+#pragma unroll
+      for (int k = 0; k < NL; k++) bx.v[k] = base[k][lane], by.v[k] = base[NL + k][lane];
+    };
+    bool ok;
+    if (flags & KZGPOT_SUBGROUP_REF) {
+      ok = in_subgroup_ref<fp>(load);
+    } else {
+      auto park = [&](const jac<fp>& q) {
+#pragma unroll
+        for (int k = 0; k < NL; k++) {
+          qpark[k][threadIdx.x] = q.x.v[k];
+          qpark[NL + k][threadIdx.x] = q.y.v[k];
+          qpark[2 * NL + k][threadIdx.x] = q.z.v[k];
+        }
+      };
+      auto load_q = [&](fp& qx, fp& qy) {
+        uint32_t lane = threadIdx.x;
+        asm volatile("" : "+v"(lane));
+#pragma unroll
+        for (int k = 0; k < NL; k++) qx.v[k] = qpark[k][lane], qy.v[k] = qpark[NL + k][lane];
+      };
+      auto load_qz = [&](fp& qz) {
+        uint32_t lane = threadIdx.x;
+        asm volatile("" : "+v"(lane));
+#pragma unroll
+        for (int k = 0; k < NL; k++) qz.v[k] = qpark[2 * NL + k][lane];
+      };
+      ok = in_subgroup_fast_g1(load, park, load_q, load_qz);
+    }
+    if (!ok) st = 5;
+  }
+  if (st) store_zero(dst, 6);
   report(i, st, first_bad, status);
 }
 
@@ -477,6 +581,10 @@ hipError_t launch_codec(CodecOp op, const void* d_in, void* d_out, uint64_t n, u
   const bool checked = !(flags & KZGPOT_NO_SUBGROUP_CHECK);
   switch (op) {
     case CodecOp::G1Decompress:
+      if (checked && !(flags & KZGPOT_SPLIT_PHASES)) {
+        hipLaunchKernelGGL(k_g1_codec, grid, block, 0, stream, in, out, n, flags, d_first_bad, d_status);
+        break;
+      }
       hipLaunchKernelGGL(k_g1_decompress, grid, block, 0, stream, in, out, n, flags, d_first_bad, d_status);
       if (checked)
         hipLaunchKernelGGL(k_g1_check<Src::ArkInPlace>, grid, block, 0, stream, in, out, n, flags, d_first_bad,

@@ -55,6 +55,14 @@ KZG_DEV void fp_zero(Fe<Tr>& r) {
   for (int i = 0; i < Tr::NL; i++) r.v[i] = 0;
 }
 
+// 2x as a VOP2 add: a wave64 v_add_u32 issues in ~2 SIMD cycles, the v_lshlrev_b32 the compiler
+// emits for x << 1 in ~4 (profiles/r02_valu_issue_microbench.txt). asm, or the compiler folds it back.
+KZG_DEV uint32_t dbl_u32(uint32_t x) {
+  uint32_t r;
+  asm("v_add_u32_e32 %0, %1, %1" : "=v"(r) : "v"(x));
+  return r;
+}
+
 // ------------------------------------------------------------------------------- multiply
 // r = a b R^-1 mod p. Requires limb-bit(a) + limb-bit(b) <= 60 (see header). Output normalized.
 template <class Tr>
@@ -126,7 +134,7 @@ KZG_DEV void fp_sqr(Fe<Tr>& r, const Fe<Tr>& a) {
   constexpr int N = Tr::NL;
   uint32_t d[N], m[N];
 #pragma unroll
-  for (int j = 0; j < N; j++) d[j] = a.v[j] << 1;
+  for (int j = 0; j < N; j++) d[j] = dbl_u32(a.v[j]);
   uint64_t acc = 0;
 #pragma unroll
   for (int i = 0; i < 2 * N - 1; i++) {
@@ -159,7 +167,7 @@ KZG_DEV void fp_add_nr(Fe<Tr>& r, const Fe<Tr>& a, const Fe<Tr>& b) {
 template <int S, class Tr>
 KZG_DEV void fp_shl_nr(Fe<Tr>& r, const Fe<Tr>& a) {  // 2^S a, limb-wise
 #pragma unroll
-  for (int i = 0; i < Tr::NL; i++) r.v[i] = a.v[i] << S;
+  for (int i = 0; i < Tr::NL; i++) r.v[i] = S == 1 ? dbl_u32(a.v[i]) : a.v[i] << S;
 }
 template <class Tr>
 KZG_DEV void fp_mul3_nr(Fe<Tr>& r, const Fe<Tr>& a) {

@@ -36,6 +36,7 @@ TAU_POWERS_G1_LENGTH = (TAU_POWERS_LENGTH << 1) - 1        # src/lib.rs:24
 
 NO_SUBGROUP_CHECK = 0x1
 SUBGROUP_REF = 0x2
+SPLIT_PHASES = 0x4  # checked G1: decompress and check as two launches (A/B of the fused kernel)
 MODE_KZG = 0
 MODE_FASTKZG = 1
 

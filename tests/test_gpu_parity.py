@@ -16,7 +16,7 @@ OPS = [("g1_decompress", 48, 96), ("g2_decompress", 96, 192), ("g1_transcode", 9
 
 
 @pytest.mark.parametrize("op,rin,rout", OPS)
-@pytest.mark.parametrize("mode", [0, 2], ids=["fast", "ref"])
+@pytest.mark.parametrize("mode", [0, 2, 4], ids=["fast", "ref", "split"])
 def test_golden_vectors_one_by_one(gpu, op, rin, rout, mode):
     for v in golden(op):
         flags = mode | (0 if v["check"] else gpu.NO_SUBGROUP_CHECK)
@@ -66,7 +66,9 @@ def test_empty_input(gpu):
         assert r.ret == 0 and r.out == b"" and r.first_bad == -1
 
 
-@pytest.mark.parametrize("mode", [0, 2], ids=["fast", "ref"])
+# modes: fused one-pass kernel (default) / split decompress + check launches (SPLIT_PHASES), each
+# with the endomorphism subgroup test or the reference's double-and-add by r (SUBGROUP_REF)
+@pytest.mark.parametrize("mode", [0, 2, 4, 6], ids=["fast", "ref", "fast-split", "ref-split"])
 def test_mixed_stream_matches_oracle(gpu, oracle_lib, mode):
     n = 3000
     data, _ = _random_stream(oracle_lib, n, seed=99 + mode, neg_every=37)

@@ -14,7 +14,8 @@ no average mixes sizes):
   * registers: the CSV's VGPR columns (rocprofv3 reports the arch VGPR field in its own units) and
     the code object's .vgpr_count / .group_segment_fixed_size / waves per SIMD, taken from
     profiles/r02_valu_mix.json (tools/valu_mix.py) so DESIGN's occupancy claims can be checked.
-bench.py reads the G1 codec entry (`k_g1_decompress` + `k_g1_check`) for `roofline.traffic` and
+bench.py reads the G1 codec entry (`k_g1_codec`, or `k_g1_decompress` + `k_g1_check` for the split
+kernels) for `roofline.traffic` and
 the per-kernel instruction counts for its `valu` roofs.
 """
 from __future__ import annotations
@@ -26,6 +27,7 @@ import json
 import os
 
 KERNELS = {
+    "k_g1_codec": "kzgpot::k_g1_codec(",
     "k_g1_decompress": "kzgpot::k_g1_decompress(",
     "k_g1_check": "kzgpot::k_g1_check<(kzgpot::Src)0>",
     "k_g2_decompress": "kzgpot::k_g2_decompress(",
@@ -103,7 +105,9 @@ def main():
             if s and c in s:
                 e[c.lower()] = s[c]
         out["kernels"][k] = e
-    if "k_g1_decompress" in out["kernels"] and "k_g1_check" in out["kernels"]:
+    if "k_g1_codec" in out["kernels"]:  # the fused one-pass kernel (default since round 2)
+        out["g1_bytes_per_point"] = out["kernels"]["k_g1_codec"]["bytes_per_point"]
+    elif "k_g1_decompress" in out["kernels"] and "k_g1_check" in out["kernels"]:
         out["g1_bytes_per_point"] = (out["kernels"]["k_g1_decompress"]["bytes_per_point"]
                                      + out["kernels"]["k_g1_check"]["bytes_per_point"])
     with open(a.out, "w") as f:
