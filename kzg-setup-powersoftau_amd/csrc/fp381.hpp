@@ -125,6 +125,40 @@ KZG_DEV void fp_mul_sum2(Fe<Tr>& r, const Fe<Tr>& a, const Fe<Tr>& b, const Fe<T
     acc >>= Tr::LB;
   }
 }
+// r = (a b + c d + e f) R^-1 mod p: three products and the m*p terms in one column scan, one
+// reduction — the folded G2 doubling's Y3 components (curve.hpp). Bounds: field_bounds_model mul_sum3.
+template <class Tr>
+KZG_DEV void fp_mul_sum3(Fe<Tr>& r, const Fe<Tr>& a, const Fe<Tr>& b, const Fe<Tr>& c, const Fe<Tr>& d,
+                         const Fe<Tr>& e, const Fe<Tr>& f) {
+  constexpr int N = Tr::NL;
+  uint32_t m[N];
+  uint64_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < 2 * N; i++) {
+    const int j0 = i < N ? 0 : i - (N - 1);
+    const int j1 = i < N ? i - 1 : N - 1;
+    uint64_t acc2 = 0, acc3 = 0, accp = 0;
+#pragma unroll
+    for (int j = j0; j <= j1; j++) {
+      acc += (uint64_t)a.v[j] * b.v[i - j];
+      acc2 += (uint64_t)c.v[j] * d.v[i - j];
+      acc3 += (uint64_t)e.v[j] * f.v[i - j];
+      accp += (uint64_t)m[j] * Tr::P[i - j];
+    }
+    if (i < N) {
+      acc += (uint64_t)a.v[i] * b.v[0];
+      acc2 += (uint64_t)c.v[i] * d.v[0];
+      acc3 += (uint64_t)e.v[i] * f.v[0];
+      acc += acc2 + acc3 + accp;
+      m[i] = ((uint32_t)acc * Tr::PINV) & Tr::MASK;
+      acc += (uint64_t)m[i] * Tr::P[0];
+    } else {
+      acc += acc2 + acc3 + accp;
+      r.v[i - N] = (uint32_t)acc & Tr::MASK;
+    }
+    acc >>= Tr::LB;
+  }
+}
 // r = a^2 R^-1 mod p: each cross product a_j a_k (j < k) once, as a_j (2 a_k), plus the squares —
 // NL(NL+1)/2 instead of NL^2 products for the a*a half (the NL^2 m*p products of the reduction
 // stay). Every column partial sum is at most fp_mul(a, a)'s, so the same bounds hold; in addition

@@ -125,6 +125,22 @@ def mul_sum2(a: V, b: V, c: V, d: V, name="mul_sum2"):
     return normalized(((a.val * b.val + c.val * d.val) * P_OVER_R + 1) * UP, name)
 
 
+def mul_sum3(a: V, b: V, c: V, d: V, e: V, f: V, name="mul_sum3"):
+    """fp_mul_sum3: a b + c d + e f with one Montgomery reduction (four mad chains per column)."""
+    carry = 0
+    for i in range(2 * NL):
+        j0 = 0 if i < NL else i - (NL - 1)
+        j1 = i if i < NL else NL - 1
+        s = sum(a.limbs[j] * b.limbs[i - j] + c.limbs[j] * d.limbs[i - j] + e.limbs[j] * f.limbs[i - j]
+                for j in range(j0, j1 + 1))
+        s += sum(LM * P_L[i - j] for j in range(j0, j1 + 1))
+        s += carry
+        if s >= 1 << 64:
+            raise BoundError(f"{name}: column {i} may reach {s.bit_length()} bits")
+        carry = s >> LB
+    return normalized(((a.val * b.val + c.val * d.val + e.val * f.val) * P_OVER_R + 1) * UP, name)
+
+
 def sqr(a: V, name="sqr"):
     """fp_sqr: same column sums as mul(a, a); the doubled operand 2 a_k must fit 32 bits."""
     if max(a.limbs) >= 1 << 31:
@@ -451,12 +467,16 @@ def jac_dbl_fp2_lz(X, Y, Z):
     d = mul2(shl2(X, 2), b, "KB_2_28", "D")
     e = norm2(mul3_2(a), "E")
     f = sqr2(e, "KB_4_28", "F")
-    c = sqr2(b, "KB_2_28", "C")
     x3 = norm2(subk2(f, shl2(d, 1), "KB_4_29", "X3"), "X3")
     t = subk2(d, x3, "KB_8_28", "D-X3")
-    y3 = mul2(e, t, "KB_16_30", "E(D-X3)")
-    y3 = norm2(subk2(y3, shl2(c, 3), "KB_16_31", "Y3"), "Y3")
-    return x3, y3, z3
+    # Y3 = E (D - X3) - 8 B^2, one three-product reduction per component
+    u = subk(normalized(0), t.c1, "KB_16_30", "-t1")
+    s = add_nr(b.c0, b.c1, "b0+b1")
+    n0 = norm(subk(normalized(0), shl(norm(subk(b.c0, b.c1, "KB_2_28", "b0-b1")), 3), "KB_64_31", "-8(b0-b1)"))
+    y0 = mul_sum3(e.c0, t.c0, e.c1, u, s, n0, "Y3.c0")
+    n1 = norm(subk(normalized(0), shl(b.c1, 3), "KB_16_31", "-8b1"))
+    y1 = mul_sum3(e.c0, t.c1, e.c1, t.c0, shl(b.c0, 1), n1, "Y3.c1")
+    return x3, V2(y0, y1), z3
 
 
 def jac_madd_fp2_lz(X, Y, Z, x2, y2):
