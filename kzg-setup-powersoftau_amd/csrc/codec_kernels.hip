@@ -108,9 +108,9 @@ __global__ void __launch_bounds__(kBlock) k_g1_decompress(const uint4* __restric
 
 // ================================================================================ fused G1 codec
 // Both phases of a checked G1 point in one lane and one launch (the default for checked
-// streams): x's canonical words go out as soon as x < p is known, the Montgomery x is parked in
-// LDS before the square root, y's canonical words go out after the sign rule and its Montgomery
-// form is parked next to x — so nothing but the ladder state is live across the subgroup test,
+// streams): x's canonical words and its Montgomery form are parked in LDS before the square root,
+// the ark record (x, y) goes out after the sign rule and y's Montgomery form is parked next to x —
+// so nothing but the ladder state is live across the subgroup test,
 // and no record is read back from HBM (48 B in + 96 B out per point, against 48 + 96 + 96 + the
 // x re-read of the split kernels). A rejected point's record is zero-filled (the split path's
 // phase 2 does the same to its poison record). 70 KB of LDS per block (base point + the second
@@ -140,7 +140,8 @@ __global__ void __launch_bounds__(kBlock) k_g1_codec(const uint4* __restrict__ i
     else if (b0 & 0x40u) st = inf_clean ? 7 : 2;  // checked stream: infinity is rejected
     else if (words_geq_p(w)) st = 3;
     greatest = (b0 & 0x20u) != 0;
-    if (st == 0) store_words(dst, w);  // ark x = the canonical x
+#pragma unroll
+    for (int k = 0; k < 12; k++) qpark[k][threadIdx.x] = w[k];  // ark x = the canonical x (qpark is free until the ladder)
     fp t, u;
     words_to_mont(t, w);
 #pragma unroll
@@ -161,6 +162,12 @@ __global__ void __launch_bounds__(kBlock) k_g1_codec(const uint4* __restrict__ i
     fp_neg_canon(nyc, yc);
     fp_select(yc, fp_lt_canon(yc, nyc) ^ greatest, yc, nyc);
     if (st == 0) {
+      words w;  // the whole 96-B record in one go: a 48-B half written long before the other costs
+      uint32_t lane = threadIdx.x;  // a partial 64-B write per half (PMC: 155 instead of 96 B/point)
+      asm volatile("" : "+v"(lane));
+#pragma unroll
+      for (int k = 0; k < 12; k++) w[k] = qpark[k][lane];
+      store_words(dst, w);
       store_canon(dst + 3, yc);
       fp_to_mont(y, yc);
 #pragma unroll
@@ -259,6 +266,7 @@ __global__ void __launch_bounds__(kBlock) k_g2_decompress(const uint4* __restric
                                                           uint64_t n, uint32_t flags,
                                                           unsigned long long* __restrict__ first_bad,
                                                           uint8_t* __restrict__ status) {
+  __shared__ uint32_t xpark[24][kBlock];  // x's canonical words across the square root (no HBM re-read)
   const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
   const bool checked = !(flags & KZGPOT_NO_SUBGROUP_CHECK);
@@ -280,6 +288,8 @@ __global__ void __launch_bounds__(kBlock) k_g2_decompress(const uint4* __restric
     else if (words_geq_p(w0) || words_geq_p(w1)) st = 3;
     is_inf = (b0 & 0xc0u) == 0xc0u && st == 0;
     greatest = (b0 & 0x20u) != 0;
+#pragma unroll
+    for (int k = 0; k < 12; k++) xpark[k][threadIdx.x] = w0[k], xpark[12 + k][threadIdx.x] = w1[k];
     fp2 x;
     words_to_mont(x.c0, w0);
     words_to_mont(x.c1, w1);
@@ -304,9 +314,10 @@ __global__ void __launch_bounds__(kBlock) k_g2_decompress(const uint4* __restric
   uint4* dst = out + i * 12;
   if (st == 0 && !is_inf) {
     words w1, w0;
-    load_be(w1, opaque(in) + i * 6);
-    load_be(w0, opaque(in) + i * 6 + 3);
-    w1[11] &= 0x1fffffffu;
+    uint32_t lane = threadIdx.x;
+    asm volatile("" : "+v"(lane));
+#pragma unroll
+    for (int k = 0; k < 12; k++) w0[k] = xpark[k][lane], w1[k] = xpark[12 + k][lane];
     fp_select(yc.c0, keep, yc.c0, nyc.c0);
     fp_select(yc.c1, keep, yc.c1, nyc.c1);
     store_words(dst, w0);
