@@ -56,9 +56,9 @@ extern "C" {
 /* Use the reference's own subgroup algorithm (ark mul_bits by r, 255-bit double-and-add) instead
  * of the endomorphism test. Same boolean for every point; ~3x slower. For cross-validation. */
 #define KZGPOT_SUBGROUP_REF 0x2u
-/* Checked G1 decompression as two launches (decompress, then the arkworks check in place on its
- * output — the split kernels) instead of the fused one-pass kernel. Same output and statuses; for
- * A/B measurement. */
+/* Checked G1 / G2 decompression as two launches (decompress, then the arkworks check in place on
+ * its output — the split kernels) instead of the fused one-pass kernel. Same output and statuses;
+ * for A/B measurement. */
 #define KZGPOT_SPLIT_PHASES 0x4u
 
 /* ---------------------------------------------------------------- hot path, host buffers */

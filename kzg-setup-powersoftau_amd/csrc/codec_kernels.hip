@@ -1,6 +1,6 @@
-// The hot path: one lane per point, decompress -> check -> arkworks emit. Checked G1 streams (the
-// headline) run both phases in ONE kernel (k_g1_codec, below); G2, unchecked G1 and the
-// KZGPOT_SPLIT_PHASES A/B mode run them as two kernels.
+// The hot path: one lane per point, decompress -> check -> arkworks emit. Checked streams (the
+// headline) run both phases in ONE kernel (k_g1_codec / k_g2_codec, below); unchecked streams run
+// phase 1 alone, and the KZGPOT_SPLIT_PHASES A/B mode runs the two phases as two kernels.
 //
 // Replaces, per point, the reference's three CPU passes:
 //   powersoftau Accumulator::deserialize → pairing into_affine_unchecked   (preprocess-kgz.rs:105)
@@ -193,11 +193,12 @@ __global__ void __launch_bounds__(kBlock) k_g1_codec(const uint4* __restrict__ i
           qpark[2 * NL + k][threadIdx.x] = q.z.v[k];
         }
       };
-      auto load_q = [&](fp& qx, fp& qy) {
+      auto load_row = [&](int src, fp& bx, fp& by) {  // src 0: P (base), 1: Q1 (qpark); wave-uniform
         uint32_t lane = threadIdx.x;
         asm volatile("" : "+v"(lane));
+        const uint32_t* b = src ? &qpark[0][0] : &base[0][0];
 #pragma unroll
-        for (int k = 0; k < NL; k++) qx.v[k] = qpark[k][lane], qy.v[k] = qpark[NL + k][lane];
+        for (int k = 0; k < NL; k++) bx.v[k] = b[k * kBlock + lane], by.v[k] = b[(NL + k) * kBlock + lane];
       };
       auto load_qz = [&](fp& qz) {
         uint32_t lane = threadIdx.x;
@@ -205,7 +206,7 @@ __global__ void __launch_bounds__(kBlock) k_g1_codec(const uint4* __restrict__ i
 #pragma unroll
         for (int k = 0; k < NL; k++) qz.v[k] = qpark[2 * NL + k][lane];
       };
-      ok = in_subgroup_fast_g1(load, park, load_q, load_qz);
+      ok = in_subgroup_fast_g1(load_row, park, load_qz);
     }
     if (!ok) st = 5;
   }
@@ -340,6 +341,97 @@ __global__ void __launch_bounds__(kBlock) k_g2_decompress(const uint4* __restric
   report(i, st, first_bad, status);
 }
 
+// ================================================================================ fused G2 codec
+// Both phases of a checked G2 point in one lane and one launch, as k_g1_codec: x's Montgomery
+// form is parked in LDS before the square root (its canonical words wait in y's slots, which are
+// free until the emit), the ark record goes out in one go after the sign rule, and y's Montgomery
+// form replaces the words. The ladder reads the base point from LDS. The split path's check
+// re-reads the 192-B record, converts four coordinates and tests the curve equation; here the
+// point is on the curve by construction (fp2_sqrt verified y^2 = x^3 + 4 (1 + u)) and only y is
+// converted. 56 KB of LDS per block.
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 2)))
+k_g2_codec(const uint4* __restrict__ in, uint4* __restrict__ out, uint64_t n, uint32_t flags,
+           unsigned long long* __restrict__ first_bad, uint8_t* __restrict__ status) {
+  __shared__ uint32_t base[4 * NL][kBlock];  // x.c0, x.c1, y.c0, y.c1 (Montgomery), limb-major
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  int st = 0;
+  bool greatest;
+  uint4* dst = out + i * 12;
+  fp2 a;
+  {
+    words w1, w0;  // wire order: x.c1 ‖ x.c0
+    load_be(w1, in + i * 6);
+    load_be(w0, in + i * 6 + 3);
+    const uint32_t b0 = w1[11] >> 24;
+    uint32_t rest = w0[11];
+#pragma unroll
+    for (int k = 0; k < 11; k++) rest |= w1[k] | w0[k];
+    const bool inf_clean = ((w1[11] & 0x3fffffffu) | rest) == 0;
+    w1[11] &= 0x1fffffffu;
+    if (!(b0 & 0x80u)) st = 1;
+    else if (b0 & 0x40u) st = inf_clean ? 7 : 2;  // checked stream: infinity is rejected
+    else if (words_geq_p(w0) || words_geq_p(w1)) st = 3;
+    greatest = (b0 & 0x20u) != 0;
+#pragma unroll
+    for (int k = 0; k < 12; k++) base[2 * NL + k][threadIdx.x] = w0[k], base[2 * NL + 12 + k][threadIdx.x] = w1[k];
+    fp2 x;
+    words_to_mont(x.c0, w0);
+    words_to_mont(x.c1, w1);
+#pragma unroll
+    for (int k = 0; k < NL; k++) base[k][threadIdx.x] = x.c0.v[k], base[NL + k][threadIdx.x] = x.c1.v[k];
+    g2_rhs(a, x);
+  }
+  {
+    fp2 y;
+    const bool on = fp2_sqrt(y, a);
+    if (st == 0 && !on) st = 4;
+    fp2 yc, nyc;
+    fp_from_mont(yc.c0, y.c0);
+    fp_from_mont(yc.c1, y.c1);
+    fp_neg_canon(nyc.c0, yc.c0);
+    fp_neg_canon(nyc.c1, yc.c1);
+    bool c1eq = true;
+#pragma unroll
+    for (int k = 0; k < NL; k++) c1eq = c1eq && (yc.c1.v[k] == nyc.c1.v[k]);
+    const bool keep = (c1eq ? fp_lt_canon(yc.c0, nyc.c0) : fp_lt_canon(yc.c1, nyc.c1)) ^ greatest;
+    if (st == 0) {
+      words w0, w1;
+      uint32_t lane = threadIdx.x;
+      asm volatile("" : "+v"(lane));
+#pragma unroll
+      for (int k = 0; k < 12; k++) w0[k] = base[2 * NL + k][lane], w1[k] = base[2 * NL + 12 + k][lane];
+      fp_select(yc.c0, keep, yc.c0, nyc.c0);
+      fp_select(yc.c1, keep, yc.c1, nyc.c1);
+      store_words(dst, w0);
+      store_words(dst + 3, w1);
+      store_canon(dst + 6, yc.c0);
+      store_canon(dst + 9, yc.c1);
+      fp_to_mont(y.c0, yc.c0);
+      fp_to_mont(y.c1, yc.c1);
+#pragma unroll
+      for (int k = 0; k < NL; k++) base[2 * NL + k][threadIdx.x] = y.c0.v[k], base[3 * NL + k][threadIdx.x] = y.c1.v[k];
+    }
+  }
+  if (st == 0) {
+    auto load = [&](fp2& bx, fp2& by) {
+      uint32_t lane = threadIdx.x;
+      asm volatile("" : "+v"(lane));  // opaque index: re-read at every use, never hoisted
+#pragma unroll
+      for (int k = 0; k < NL; k++) {
+        bx.c0.v[k] = base[k][lane];
+        bx.c1.v[k] = base[NL + k][lane];
+        by.c0.v[k] = base[2 * NL + k][lane];
+        by.c1.v[k] = base[3 * NL + k][lane];
+      }
+    };
+    const bool ok = (flags & KZGPOT_SUBGROUP_REF) ? in_subgroup_ref<fp2>(load) : in_subgroup_fast_g2(load);
+    if (!ok) st = 5;
+  }
+  if (st) store_zero(dst, 12);
+  report(i, st, first_bad, status);
+}
+
 // ================================================================================ phase 2
 // ark-ec 0.2 deserialize_uncompressed on one record, then serialize_uncompressed.
 //   Src::ArkInPlace : the record is phase 1's output (ark LE, x ‖ y)           — decompress path
@@ -441,11 +533,12 @@ __global__ void __launch_bounds__(kBlock) k_g1_check(const uint4* __restrict__ i
           qpark[2 * NL + k][threadIdx.x] = q.z.v[k];
         }
       };
-      auto load_q = [&](fp& qx, fp& qy) {
+      auto load_row = [&](int src, fp& bx, fp& by) {  // src 0: P (base), 1: Q1 (qpark); wave-uniform
         uint32_t lane = threadIdx.x;
         asm volatile("" : "+v"(lane));
+        const uint32_t* b = src ? &qpark[0][0] : &base[0][0];
 #pragma unroll
-        for (int k = 0; k < NL; k++) qx.v[k] = qpark[k][lane], qy.v[k] = qpark[NL + k][lane];
+        for (int k = 0; k < NL; k++) bx.v[k] = b[k * kBlock + lane], by.v[k] = b[(NL + k) * kBlock + lane];
       };
       auto load_qz = [&](fp& qz) {
         uint32_t lane = threadIdx.x;
@@ -453,7 +546,7 @@ __global__ void __launch_bounds__(kBlock) k_g1_check(const uint4* __restrict__ i
 #pragma unroll
         for (int k = 0; k < NL; k++) qz.v[k] = qpark[2 * NL + k][lane];
       };
-      ok = in_subgroup_fast_g1(load, park, load_q, load_qz);
+      ok = in_subgroup_fast_g1(load_row, park, load_qz);
     }
     if (!ok) st = 5;
   }
@@ -602,6 +695,10 @@ hipError_t launch_codec(CodecOp op, const void* d_in, void* d_out, uint64_t n, u
                            d_status);
       break;
     case CodecOp::G2Decompress:
+      if (checked && !(flags & KZGPOT_SPLIT_PHASES)) {
+        hipLaunchKernelGGL(k_g2_codec, grid, block, 0, stream, in, out, n, flags, d_first_bad, d_status);
+        break;
+      }
       hipLaunchKernelGGL(k_g2_decompress, grid, block, 0, stream, in, out, n, flags, d_first_bad, d_status);
       if (checked)
         hipLaunchKernelGGL(k_g2_check<Src::ArkInPlace>, grid, block, 0, stream, in, out, n, flags, d_first_bad,

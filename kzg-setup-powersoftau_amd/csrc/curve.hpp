@@ -309,23 +309,29 @@ KZG_DEV bool in_subgroup_ref(Load&& load) {
 // on which Q1 = [|u|] P = (X : Y : Z) is the AFFINE point (X, Y): a = 0 and neither formula reads
 // b, so its 5 additions are mixed additions (8M + 3S) instead of Jacobian ones (12M + 4S), and
 // [|u|] iota(Q1) = (X' : Y' : Z') is (X' : Y' : Z' Z) on E. Q1 = O (Z = 0) still ends in O.
-// park(q1) stores Q1; load_q(x, y) / load_qz(z) fetch it back (the kernel parks it in LDS).
-template <typename Load, typename Park, typename LoadQ, typename LoadQZ>
-KZG_DEV bool in_subgroup_fast_g1(Load&& load, Park&& park, LoadQ&& load_q, LoadQZ&& load_qz) {
-  jac<fp> q2;
-  {
-    jac<fp> q1;
-    mul_abs_u_affine(q1, load);
-    park(q1);
+// load_row(0, x, y) fetches P, park(q1) stores Q1, load_row(1, x, y) / load_qz(z) fetch it back
+// (the kernels park both in LDS). The two ladders are ONE copy of the ladder code, run twice
+// with a wave-uniform source row: each copy is ~25 KB of straight-line doubling code, and two
+// of them plus the square root's loop overflow the 64 KB instruction cache a CU pair shares.
+template <typename LoadRow, typename Park, typename LoadQZ>
+KZG_DEV bool in_subgroup_fast_g1(LoadRow&& load_row, Park&& park, LoadQZ&& load_qz) {
+  jac<fp> q;
+  int src = 0;
+  auto load = [&](fp& bx, fp& by) { load_row(src, bx, by); };
+#pragma unroll 1
+  for (int pass = 0; pass < 2; pass++) {
+    src = __builtin_amdgcn_readfirstlane(pass);
+    mul_abs_u_affine(q, load);
+    if (pass == 0) park(q);
   }
-  mul_abs_u_affine(q2, load_q);
   {
     fp z;
     load_qz(z);
-    fp_mul(q2.z, q2.z, z);
+    fp_mul(q.z, q.z, z);
   }
+  jac<fp>& q2 = q;
   fp x, y, beta;
-  load(x, y);
+  load_row(0, x, y);
   fp_set(beta, FP_BETA);
   fp_mul(x, x, beta);
   fp_neg(y, y);

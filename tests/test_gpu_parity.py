@@ -79,6 +79,19 @@ def test_mixed_stream_matches_oracle(gpu, oracle_lib, mode):
     assert (r.ret, r.first_bad) == (ret, fb)
 
 
+@pytest.mark.parametrize("mode", [0, 2, 4, 6], ids=["fast", "ref", "fast-split", "ref-split"])
+def test_g2_mixed_stream_matches_oracle(gpu, oracle_lib, mode):
+    """G2 through the fused codec and the split pair: every checked golden vector class (valid,
+    non-residue, x >= p, infinity, bad flags, off-subgroup) shuffled into one 700-point stream."""
+    vecs = [bytes.fromhex(v["in"]) for v in golden("g2_decompress") if v["check"]]
+    rng = random.Random(7 + mode)
+    n = 700
+    data = b"".join(rng.choice(vecs) for _ in range(n))
+    r = gpu.run_codec("g2_decompress", data, mode, want_status=True)
+    out, st, fb, ret = oracle_run(oracle_lib, "g2_decompress", data, n)
+    assert r.status == st and r.out == out and (r.ret, r.first_bad) == (ret, fb)
+
+
 def test_no_subgroup_check_mode(gpu, oracle_lib):
     n = 2000
     data, _ = _random_stream(oracle_lib, n, seed=5, neg_every=41)
