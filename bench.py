@@ -39,6 +39,7 @@ ALG_BYTES = {"g1": 144, "g2": 288, "bn254": 96}  # bytes read + 
 # kernel -> its name in profiles/r02_valu_mix.json (demangled; the check kernels' Src 0 = ArkInPlace)
 MIX_NAMES = {"k_g1_codec": "kzgpot::k_g1_codec(",
              "k_g1_decompress": "kzgpot::k_g1_decompress(", "k_g1_check": "kzgpot::k_g1_check<(kzgpot::Src)0>",
+             "k_g2_codec": "kzgpot::k_g2_codec(",
              "k_g2_decompress": "kzgpot::k_g2_decompress(", "k_g2_check": "kzgpot::k_g2_check<(kzgpot::Src)0>",
              "k_bn254_g1_decompress": "kzgpot::k_bn254_g1_decompress("}
 RECORDS = {"g1": (48, 96, "g1_decompress"), "g2": (96, 192, "g2_decompress"),
@@ -64,7 +65,7 @@ def parse():
     ap.add_argument("--gather-chunks", type=int, default=8,
                     help="N > 1: chunks per rank; each chunk's all-gather overlaps the next chunk's decode")
     ap.add_argument("--split-phases", action="store_true",
-                    help="G1: decompress and check as two launches (KZGPOT_SPLIT_PHASES) instead of the fused kernel")
+                    help="G1 and G2: decompress and check as two launches (KZGPOT_SPLIT_PHASES) instead of the fused kernels")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--oracle-sample-runs", type=int, default=64,
                     help="runs of 256 output records (+ the last 256) re-decoded by the C oracle")
@@ -463,10 +464,10 @@ def main():
             except (OSError, RuntimeError) as e:  # reported in the line; the torch path is the same layout
                 print(f"warning: library communicator unavailable ({e}); torch.distributed gathers", file=sys.stderr)
                 gather_impl = f"torch.distributed (library communicator failed: {e})"
-    g1_flags = 0x4 if args.split_phases else 0  # KZGPOT_SPLIT_PHASES
+    g1_flags = 0x4 if args.split_phases else 0  # KZGPOT_SPLIT_PHASES (applies to G1 and G2)
     g1_kernels = ["k_g1_decompress", "k_g1_check"] if args.split_phases else ["k_g1_codec"]
     g1 = Sharded("g1", n1, args.seed, args.gather_chunks, rank, world, gather, dev, verify, comm, g1_flags)
-    g2 = Sharded("g2", n2, args.seed + 1, 1, rank, world, gather, dev, verify, comm)  # 2^16 points: one chunk
+    g2 = Sharded("g2", n2, args.seed + 1, 1, rank, world, gather, dev, verify, comm, g1_flags)  # 2^16 points: one chunk
     torch.cuda.synchronize()
     t_gen = time.perf_counter() - t_gen
 
@@ -554,13 +555,13 @@ def main():
         o31 = torch.empty(n3 * 96, dtype=torch.uint8, device=dev)
         o32 = torch.empty(n3 * 192, dtype=torch.uint8, device=dev)
         k3 = torch.empty(2, dtype=torch.int64, device=dev)
-        D.codec_dev("g1_decompress", c31, o31, k3[0:1])
-        D.codec_dev("g2_decompress", c32, o32, k3[1:2])
+        D.codec_dev("g1_decompress", c31, o31, k3[0:1], g1_flags)
+        D.codec_dev("g2_decompress", c32, o32, k3[1:2], g1_flags)
         ce = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
         ce[0].record()
-        D.codec_dev("g1_decompress", c31, o31, k3[0:1])
+        D.codec_dev("g1_decompress", c31, o31, k3[0:1], g1_flags)
         ce[1].record()
-        D.codec_dev("g2_decompress", c32, o32, k3[1:2])
+        D.codec_dev("g2_decompress", c32, o32, k3[1:2], g1_flags)
         ce[2].record()
         torch.cuda.synchronize()
         g1c, g2c = ce[0].elapsed_time(ce[1]), ce[1].elapsed_time(ce[2])
@@ -569,7 +570,8 @@ def main():
             "g1_ms": g1c, "g2_ms": g2c, "points_per_s": 2 * n3 / ((g1c + g2c) * 1e-3),
             "g2_ns_per_point": g2c * 1e6 / n3,
             "g2_valu": valu_roofline(load_json("pmc_traffic.json"), load_json("r02_valu_mix.json"),
-                                     ["k_g2_decompress", "k_g2_check"], n3, g2c),
+                                     ["k_g2_decompress", "k_g2_check"] if args.split_phases else ["k_g2_codec"],
+                                     n3, g2c),
             "verified_bit_exact": bool(D.read_key(k3[0:1]) == KD.NO_BAD and D.read_key(k3[1:2]) == KD.NO_BAD
                                        and torch.equal(o31, x31) and torch.equal(o32, x32))}
         del c31, x31, c32, x32, o31, o32

@@ -30,6 +30,7 @@ KERNELS = {
     "k_g1_codec": "kzgpot::k_g1_codec(",
     "k_g1_decompress": "kzgpot::k_g1_decompress(",
     "k_g1_check": "kzgpot::k_g1_check<(kzgpot::Src)0>",
+    "k_g2_codec": "kzgpot::k_g2_codec(",
     "k_g2_decompress": "kzgpot::k_g2_decompress(",
     "k_g2_check": "kzgpot::k_g2_check<(kzgpot::Src)0>",
     "k_g1_load": "kzgpot::k_load<2, 256>",
