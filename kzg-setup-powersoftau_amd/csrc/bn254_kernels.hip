@@ -9,7 +9,8 @@
 //   else get_point_from_x(x, PositiveY): y = sqrt(x^3 + 3) (none → NotOnCurve), keep y if
 //   (y < -y) XOR PositiveY else -y; subgroup check: BN254 G1 has cofactor 1, so every curve
 //   point passes (ark's mul_bits(r) test is identically true there and is not run).
-// One lane per point; 32 B in + 64 B out against one (p-3)/4 exponentiation over a 10-limb field.
+// One lane per point; 32 B in + 64 B out against one (p-3)/4 exponentiation over a 9 x 29-bit-limb
+// field (81 products per multiply instead of 100 with 10 x 28-bit limbs).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 

@@ -1,9 +1,9 @@
 // Prime-field arithmetic for gfx950 (CDNA4), one field element per lane — generic over the field
 // (traits struct: BlsFp = BLS12-381 Fq, Bn254Fp = BN254 Fq; tools/gen_constants.py).
 //
-// Representation: NL limbs of 28 bits, each held in a 32-bit VGPR, Montgomery form with
-// R = 2^(28 NL) (BLS12-381: 14 limbs, R = 2^392; BN254: 10 limbs, R = 2^280). The 4 spare bits
-// per limb are the point of the design:
+// Representation: NL limbs of LB bits, each held in a 32-bit VGPR, Montgomery form with
+// R = 2^(LB NL) (BLS12-381: 14 x 28 bits, R = 2^392; BN254: 9 x 29 bits, R = 2^261). The spare
+// bits per limb are the point of the design (numbers below for BLS12-381's 4):
 //
 //  * Multiply (fp_mul): finely-integrated product scanning where every column sum fits ONE
 //    64-bit accumulator — up to 14 products a_j b_k < 2^60 (operand limbs < 2^30 / 2^32 x 2^28)
