@@ -23,13 +23,41 @@
 
 namespace kzgpot {
 
-// canonical words (< p) -> ark Montgomery words: x 2^384 mod p (one multiply + one conditional
-// subtraction: the product of a canonical x and FP_ARK_R is < 2p, tests/test_field_bounds.py)
+// canonical words (< p) -> ark Montgomery words: x 2^384 mod p, a multiplication by a CONSTANT,
+// so the reduction is folded into precomputed constants instead of a full Montgomery multiply:
+//   S = sum_k x_k C_k,  C_k = 2^(384 + 56 + 32 k) mod p  (FP_ARK_WORD: the 12 input words times
+//       14-limb constants — 168 single-mad columns, each < 12 x 2^32 x 2^28 < 2^63.6),
+//   then two Montgomery digit steps divide by 2^56: (S + m0 p + m1 p 2^28) / 2^56 = x 2^384
+//   (mod p), and S < 12 x 2^32 p makes it < 1.000001 p, so one conditional subtraction finishes.
+// 196 product mads and no word <-> limb conversion of the input, against fp_from_words + a
+// 392-mad fp_mul by 2^384 R. Any 384-bit input keeps every bound (the caller rejects x >= p).
 KZG_DEV void words_to_ark_mont(words& out, const words& w) {
-  fp x, k;
-  fp_from_words(x, w);
-  fp_set(k, FP_ARK_R);
-  fp_mul(x, x, k);
+  constexpr int N = BlsFp::NL;
+  uint64_t col[N + 1];
+#pragma unroll
+  for (int j = 0; j < N; j++) {
+    uint64_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 12; k++) acc += (uint64_t)w[k] * FP_ARK_WORD[k][j];
+    col[j] = acc;
+  }
+  col[N] = 0;
+#pragma unroll
+  for (int s = 0; s < 2; s++) {  // col[s] becomes a multiple of 2^28 and its carry moves up
+    const uint32_t m = ((uint32_t)col[s] * BlsFp::PINV) & BlsFp::MASK;
+#pragma unroll
+    for (int j = 0; j < N; j++) col[s + j] += (uint64_t)m * BlsFp::P[j];
+    col[s + 1] += col[s] >> BlsFp::LB;
+  }
+  fp x;
+  uint64_t c = 0;
+#pragma unroll
+  for (int k = 0; k < N - 1; k++) {
+    c += col[k + 2];
+    x.v[k] = (uint32_t)c & BlsFp::MASK;
+    c >>= BlsFp::LB;
+  }
+  x.v[N - 1] = (uint32_t)c;
   fp_reduce_once(x, x);
   fp_to_words(out, x);
 }

@@ -4,6 +4,8 @@ tests/field_bounds_model.py mirrors csrc/fp381.hpp + csrc/curve.hpp with exact i
 every fp_mul column sum is checked < 2^64, every limb < 2^32, every borrowed constant dominates
 its subtrahend limb by limb, and the ladder states are shown to live in a bound set closed under
 the ladder steps (so the proof covers all 2^64 / 2^255 steps, every input point)."""
+import os
+import random
 from fractions import Fraction
 
 import pytest
@@ -153,10 +155,61 @@ def test_synth_madd_chain():
     M.from_mont_ok(M.mul(Y, M.mul(z2, zi)), "y")
 
 
+def _ark_word_consts():
+    """FP_ARK_WORD as bls12_381_consts.hpp holds it, checked against its definition."""
+    import re
+
+    text = open(os.path.join(os.path.dirname(__file__), "..", "kzg-setup-powersoftau_amd", "csrc",
+                             "bls12_381_consts.hpp")).read()
+    body = re.search(r"FP_ARK_WORD\[12\]\[14\] = \{(.*?)\};", text).group(1)
+    rows = [[int(v.strip().rstrip("u"), 16) for v in r.split(",")] for r in re.findall(r"\{([^{}]*)\}", body)]
+    p, mask = M.P, (1 << 28) - 1
+    for k, row in enumerate(rows):
+        assert row == [((1 << (384 + 56 + 32 * k)) % p >> (28 * j)) & mask for j in range(14)]
+    return rows
+
+
 def test_loader_conversion():
-    """load_kernels.hip words_to_ark_mont: canonical x (< p) times FP_ARK_R, one reduction."""
-    k = M.const(M.C["FP_ARK_R"])
-    M.reduce_once_ok(M.mul(M.normalized(1), k))
+    """load_kernels.hip words_to_ark_mont: S = sum_k x_k C_k over the 12 input words, two
+    Montgomery digit steps, one conditional subtraction. Worst case over ANY 384-bit input (every
+    word 2^32 - 1, every digit m < 2^28): no 64-bit column overflows and the value stays < 2p;
+    then the exact device steps on random and edge inputs reproduce x 2^384 mod p."""
+    C = _ark_word_consts()
+    p = M.P
+    pl = [(p >> (28 * j)) & ((1 << 28) - 1) for j in range(14)]
+    wmax, mmax = (1 << 32) - 1, (1 << 28) - 1
+    col = [sum(wmax * C[k][j] for k in range(12)) for j in range(14)] + [0]
+    for s in range(2):  # digit steps: m p added, then the column's carry (< col >> 28) moves up
+        for j in range(14):
+            col[s + j] += mmax * pl[j]
+        col[s + 1] += col[s] >> 28
+    assert max(col) < 1 << 64
+    c = 0
+    for k in range(13):  # normalization carries
+        c += col[k + 2]
+        assert c < 1 << 64
+        c >>= 28
+    assert c < 1 << 32
+    # value: S < 12 2^32 p, so (S + m0 p + m1 p 2^28) / 2^56 < 2p for every input
+    assert (12 * (1 << 32) * p + mmax * p + mmax * p * (1 << 28)) < 2 * p * (1 << 56)
+
+    pinv = (-pow(p, -1, 1 << 28)) % (1 << 28)
+    rng = random.Random(384)
+    for i in range(3000):
+        x = [0, 1, p - 1, p, (1 << 384) - 1][i] if i < 5 else (rng.randrange(p) if i % 4 else rng.randrange(1 << 384))
+        w = [(x >> (32 * k)) & 0xFFFFFFFF for k in range(12)]
+        col = [sum(w[k] * C[k][j] for k in range(12)) for j in range(14)] + [0]
+        for s in range(2):
+            m = ((col[s] & 0xFFFFFFFF) * pinv) & ((1 << 28) - 1)
+            for j in range(14):
+                col[s + j] += m * pl[j]
+            assert col[s] & ((1 << 28) - 1) == 0
+            col[s + 1] += col[s] >> 28
+        v = sum(col[k + 2] << (28 * k) for k in range(13))
+        assert v < 2 * p
+        v = v - p if v >= p else v
+        if x < p:
+            assert v == x * (1 << 384) % p
 
 
 @pytest.fixture

@@ -201,3 +201,37 @@ def test_fuzz_bn254_decompress(gpu):
     bad = [i for i, s in enumerate(want_st) if s]
     assert r.first_bad == (bad[0] if bad else -1)
     assert 300 < want_st.count(0) and want_st.count(4) > 300
+
+
+@pytest.mark.parametrize("g2", [False, True], ids=["g1", "g2"])
+def test_fuzz_loader(gpu, g2):
+    """load_kzg_setup's per-point work (ark deserialize_unchecked: coordinates < p, SWFlags, x 2^384
+    into ark Montgomery form) on random records — random canonical coordinates (no curve needed),
+    coordinates >= p and every flag combination on y's top byte — against the Python oracle."""
+    O = pytest.importorskip("kzgpot_oracle")
+    rng = random.Random(200 + g2)
+    nc = 4 if g2 else 2
+    recs = []
+    for i in range(3000 if not g2 else 1500):
+        k = rng.randrange(100)
+        coords = [_rand_fp(rng) for _ in range(nc)]
+        if i < 4:
+            coords = [[0, 1, P - 1, (1 << 381) - 1][i]] * nc
+        elif k < 5:
+            coords[rng.randrange(nc)] = P + rng.randrange(1 << 40)
+        b = bytearray(b"".join(c.to_bytes(48, "little") for c in coords))
+        if k >= 90 or (i >= 4 and i % 13 == 0):
+            b[-1] |= rng.choice([0x40, 0x80, 0xC0])  # Infinity / PositiveY / both (UnexpectedFlags)
+        recs.append(bytes(b))
+    data = b"".join(recs)
+    r = gpu.deserialize_unchecked(data, g2=g2, want_status=True)
+    fn = O.g2_deserialize_unchecked_point if g2 else O.g1_deserialize_unchecked_point
+    rout = 200 if g2 else 104
+    want_st, want_out = [], []
+    for rec in recs:
+        st, out = fn(rec)
+        want_st.append(st)
+        want_out.append(out if st == 0 else bytes(rout))
+    assert list(r.status) == want_st
+    assert r.out == b"".join(want_out)
+    assert want_st.count(0) > 1000 if not g2 else want_st.count(0) > 500

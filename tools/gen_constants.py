@@ -191,6 +191,11 @@ def main():
         "// BLS12-381 curve constants (Montgomery form of BlsFp unless noted)",
         arr("FP_FOUR", limbs28(mont(4))),
         arr("FP_ARK_R", limbs28((1 << 384) * RM % P), "2^384 R mod p: fp_mul(x, .) = x 2^384 (ark-ff Montgomery form)"),
+        "// 2^(384 + 56 + 32 k) mod p, k = 0..11: x 2^384 mod p = (sum_k x_k FP_ARK_WORD[k]) 2^-56 for the",
+        "// 32-bit words x_k of x (the loader's canonical -> ark Montgomery conversion, load_kernels.hip)",
+        "static constexpr uint32_t FP_ARK_WORD[12][14] = {"
+        + ", ".join("{" + ", ".join(f"0x{v:08x}u" for v in limbs28((1 << (384 + 56 + 32 * k)) % P)) + "}"
+                    for k in range(12)) + "};",
         arr("FP_INV2", limbs28(mont(inv2))),
         arr("FP_BETA", limbs28(mont(beta))),
         arr("FP_PSI_CX1", limbs28(mont(cx[1]))),
