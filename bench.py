@@ -265,6 +265,24 @@ def all_ok(ok, world, dev):
     return ok
 
 
+FALLBACKS = []  # gather-path fallbacks taken during warm-up (reported in the JSON line)
+
+
+def lib_to_torch_gather(streams, err):
+    """Warm-up insurance for the multi-GPU run: if kzgpot_decode_allgather_dev fails, finish with
+    torch.distributed's all-gathers over the same block-cyclic layout (identical blocks when n
+    splits into world x chunks equal blocks, as every bench stream does). Returns False if a
+    stream cannot switch."""
+    switch = [s for s in streams if s.comm is not None]
+    if not switch or any(s.n % (s.world * s.chunks) for s in switch):
+        return False
+    for s in switch:
+        s.comm = None
+    FALLBACKS.append(f"library decode_allgather failed in warm-up ({err}); torch.distributed gathers")
+    print(f"warning: {FALLBACKS[-1]}", file=sys.stderr)
+    return True
+
+
 def timed(streams, steps, warmup, world, dev, verify):
     """W untimed warm-up steps, (verification), then EXACTLY `steps` steps bracketed by a barrier +
     synchronize; returns (max-over-ranks seconds, per-step event marks, verified)."""
@@ -278,8 +296,13 @@ def timed(streams, steps, warmup, world, dev, verify):
         for w in works:
             w.wait()  # the current stream waits for the collectives
 
-    for _ in range(warmup):
-        step(None)
+    for i in range(warmup):
+        try:
+            step(None)
+        except RuntimeError as e:  # the library's decode + RCCL gather failed on this rank
+            if i or not lib_to_torch_gather(streams, e):
+                raise
+            step(None)
     torch.cuda.synchronize()
     verified = None
     if verify:
@@ -605,7 +628,8 @@ def main():
                             "points -> arkworks uncompressed, subgroup-checked"
                             + (f", block-cyclic shards, RCCL all-gather to one contiguous buffer pipelined in "
                                f"{args.gather_chunks} chunks" if gather else ""),
-                "g1_points": n1, "g2_points": n2, "parallelism": f"shard{world}", "gather_impl": gather_impl,
+                "g1_points": n1, "g2_points": n2, "parallelism": f"shard{world}",
+                "gather_impl": gather_impl if not FALLBACKS else FALLBACKS[0],
                 "subgroup_test": "endomorphism (phi/psi), bit-exact accept/reject vs ark mul_bits(r)",
             },
             "roofline": {

@@ -191,3 +191,22 @@ def test_library_layout_covers_every_point(kzgpot_mod, n, world, chunks):
     for c in range(chunks):  # chunk c = blocks c*world .. c*world + world - 1, contiguous
         starts = sorted(KD.lib_local_ranges(n, r, world, chunks)[c][0] for r in range(world)) if b else []
         assert starts == [(c * world + r) * b for r in range(world)] if b else True
+
+
+def test_bench_lib_gather_fallback():
+    """bench.py's warm-up insurance: a failing library decode_allgather switches every stream to
+    the torch.distributed gathers over the same block-cyclic layout — only when the blocks are
+    identical (n splits into world x chunks equal blocks)."""
+    import types
+
+    import bench
+
+    mk = lambda n, world, chunks: types.SimpleNamespace(n=n, world=world, chunks=chunks, comm=object())
+    streams = [mk(1 << 27, 8, 8), mk(1 << 16, 8, 1)]
+    bench.FALLBACKS.clear()
+    assert bench.lib_to_torch_gather(streams, RuntimeError("x"))
+    assert all(s.comm is None for s in streams) and len(bench.FALLBACKS) == 1
+    assert not bench.lib_to_torch_gather(streams, RuntimeError("again"))  # nothing left to switch
+    ragged = [mk((1 << 20) + 3, 4, 8)]
+    assert not bench.lib_to_torch_gather(ragged, RuntimeError("x")) and ragged[0].comm is not None
+    bench.FALLBACKS.clear()
