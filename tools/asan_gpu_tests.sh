@@ -1,0 +1,20 @@
+#!/usr/bin/env bash
+# Host-side AddressSanitizer pass over the library's host code (C ABI, chunk pipelines, preprocess
+# threads, file streaming, BLAKE2b, loaders, communicator) while the GPU tests drive it.
+# Build first on the CPU: make -C kzg-setup-powersoftau_amd asan. Device code is not instrumented.
+set -uo pipefail
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+mkdir -p "$ROOT/gpurun_out"
+ASANRT=$(ls /opt/rocm/lib/llvm/lib/clang/*/lib/linux/libclang_rt.asan-x86_64.so | head -1)
+export KZGPOT_LIB=$ROOT/kzg-setup-powersoftau_amd/build/asan/libkzgpot.so
+export ASAN_OPTIONS=detect_leaks=0:abort_on_error=0:halt_on_error=1:log_path=$ROOT/gpurun_out/asan
+# torch's GPU initialisation does not survive the preloaded runtime (its dlopen of
+# libcaffe2_nvrtc fails), so the tests that drive the library through torch tensors are left out:
+# everything here goes through the C ABI's host-buffer entry points, the CLI binaries aside.
+LD_PRELOAD=$ASANRT timeout -k 10 600 python -u -m pytest tests/test_gpu_preprocess.py tests/test_gpu_parity.py \
+  tests/test_gpu_fuzz.py -q --timeout 300 --timeout-method thread \
+  -k "not current_device_is_restored and not load_dev_api and not bn254_synth_round_trip" \
+  > "$ROOT/gpurun_out/asan_pytest.txt" 2>&1
+rc=$?
+ls "$ROOT"/gpurun_out/asan* >/dev/null 2>&1
+exit $rc
