@@ -32,7 +32,9 @@ def main():
     lib = _lib.load()
     out = ctypes.create_string_buffer(n * 96)
     fb = ctypes.c_int64()
-    lib.kzgpot_g1_decompress(host_in.ctypes.data, ctypes.c_size_t(1 << 16), out, 0, ctypes.byref(fb))  # warm
+    t = time.perf_counter()  # warm: two full 2^21-point chunks size both slots' staging
+    lib.kzgpot_g1_decompress(host_in.ctypes.data, ctypes.c_size_t(min(n, 1 << 22)), out, 0, ctypes.byref(fb))
+    first_s = time.perf_counter() - t
     t = time.perf_counter()
     rc = lib.kzgpot_g1_decompress(host_in.ctypes.data, ctypes.c_size_t(n), out, 0, ctypes.byref(fb))
     host_s = time.perf_counter() - t
@@ -45,7 +47,7 @@ def main():
     D.codec_dev("g1_decompress", comp, d_out, key)
     torch.cuda.synchronize()
     dev_s = time.perf_counter() - t
-    print(json.dumps({"points": n, "host_api_s": host_s, "host_api_points_per_s": n / host_s,
+    print(json.dumps({"points": n, "first_call_2e22_s": first_s, "host_api_s": host_s, "host_api_points_per_s": n / host_s,
                       "device_resident_s": dev_s, "device_points_per_s": n / dev_s,
                       "pcie_overhead_frac": host_s / dev_s - 1, "bit_exact": ok, "kzgpot": kzgpot.version()}))
 
