@@ -26,7 +26,7 @@ def golden(name):
 @pytest.fixture(scope="session")
 def oracle_lib():
     """The C restatement of the reference (test infrastructure only)."""
-    path = os.path.join(ROOT, "oracle", "_build", "libkzgpot_oracle.so")
+    path = os.environ.get("KZGPOT_ORACLE_LIB", os.path.join(ROOT, "oracle", "_build", "libkzgpot_oracle.so"))
     if not os.path.exists(path):
         subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True)
     lib = ctypes.CDLL(path)
