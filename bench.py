@@ -134,7 +134,7 @@ def pmc_traffic(pmc, n_g1_local):
         return None
 
 
-def valu_roofline(pmc, mix, kernels, points, ms):
+def valu_roofline(pmc, mix, kernels, points, ms, clock=None):
     """Integer-VALU roof of a kernel group: PMC SQ_INSTS_VALU per wave (the instruction stream one
     lane runs for its point) x waves / the event-timed launch time, against the SIMDs' issue rate
     for THAT instruction mix — each opcode priced at its measured SIMD cycles per wave64
@@ -151,8 +151,10 @@ def valu_roofline(pmc, mix, kernels, points, ms):
     avg_cost = sum(i * c for i, c in zip(insts, costs)) / per_pt
     peak = SIMDS * CLOCK_HZ / avg_cost
     achieved = per_pt * (points / 64) / (ms * 1e-3)
+    at_clock = {} if not clock else {
+        "frac_at_measured_clock": achieved / (SIMDS * clock["mean"] * 1e6 / avg_cost), "measured_clock_mhz": clock["mean"]}
     return {"kernels": kernels, "valu_instr_per_point": per_pt, "avg_simd_cycles_per_instr": avg_cost,
-            "achieved_wave_instr_per_s": achieved, "peak_wave_instr_per_s": peak, "frac": achieved / peak,
+            "achieved_wave_instr_per_s": achieved, "peak_wave_instr_per_s": peak, "frac": achieved / peak, **at_clock,
             "source": "instruction counts: profiles/pmc_traffic.json (SQ_INSTS_VALU); per-opcode SIMD cycles: "
                       "profiles/r02_valu_issue_microbench.txt weighted by profiles/r02_valu_mix.json; "
                       "peak = 1024 SIMDs x 2.4 GHz / avg cycles; time: this run"}
@@ -266,6 +268,7 @@ def all_ok(ok, world, dev):
 
 
 FALLBACKS = []  # gather-path fallbacks taken during warm-up (reported in the JSON line)
+LAST_CLOCK = {}  # average shader clock over the last timed region (kzgpot.device.clock_mhz)
 
 
 def lib_to_torch_gather(streams, err):
@@ -288,6 +291,7 @@ def timed(streams, steps, warmup, world, dev, verify):
     synchronize; returns (max-over-ranks seconds, per-step event marks, verified)."""
     import torch
     import torch.distributed as dist
+    from kzgpot import device as D
 
     def step(marks):
         works = []
@@ -314,12 +318,15 @@ def timed(streams, steps, warmup, world, dev, verify):
         dist.barrier()
     torch.cuda.synchronize()
     ev = []
+    probe0 = D.clock_probe(dev)  # shader-clock counters at the start of the timed steps (a ~µs kernel)
     t0 = time.perf_counter()
     for _ in range(steps):
         marks = []
         step(marks)
         ev.append(marks)
+    probe1 = D.clock_probe(dev)  # ... and after them, on the same stream
     torch.cuda.synchronize()
+    LAST_CLOCK["mhz"] = D.clock_mhz(probe0, probe1)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -495,6 +502,7 @@ def main():
     t_gen = time.perf_counter() - t_gen
 
     elapsed, ev, verified = timed([g1, g2], args.steps, args.warmup, world, dev, verify)
+    clock = LAST_CLOCK.get("mhz")
     bad = KD.allreduce_min_key(min(g1.bad_key(), g2.bad_key()), dev) if world > 1 else min(g1.bad_key(), g2.bad_key())
     sample = None
     if verify and rank == 0 and (gather or world == 1):
@@ -645,7 +653,12 @@ def main():
                 "algorithmic_bytes_per_point": ALG_BYTES["g1"],
                 "note": "integer-VALU bound, not HBM: see valu",
             },
-            "valu": valu_roofline(pmc, load_json("r02_valu_mix.json"), g1_kernels, g1.m, g1_ms),
+            "valu": valu_roofline(pmc, load_json("r02_valu_mix.json"), g1_kernels, g1.m, g1_ms, clock),
+            "clock_mhz": None if clock is None else {
+                "mean": clock["mean"], "min": min(clock["per_xcd"].values()), "max": max(clock["per_xcd"].values()),
+                "xcds": len(clock["per_xcd"]),
+                "source": "s_memtime / s_memrealtime of each XCD at the start and end of the timed steps "
+                          "(kzgpot_synth_clock_probe); explains box-to-box spread at the same code"},
             "kernels_ms": {"g1_codec": g1_ms, "g2_codec": g2_ms},
             "verified_bit_exact": verified,
             "oracle_sample_check": sample,

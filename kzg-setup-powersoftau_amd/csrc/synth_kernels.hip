@@ -266,10 +266,28 @@ __global__ void __launch_bounds__(kSynthBlock) k_synth_bn254(uint64_t seed, uint
   }
 }
 
+// Clock probe for bench.py (measurement only, not the product): each of the launch's blocks records
+// its XCD (HW_REG_XCC_ID), the shader-clock counter (s_memtime) and the 100 MHz real-time counter
+// (s_memrealtime). Two probes around a timed region give each XCD's average shader clock over it.
+__global__ void k_clock_probe(unsigned long long* out) {
+  if (threadIdx.x) return;
+  uint32_t xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  const uint64_t t = __builtin_amdgcn_s_memtime(), r = __builtin_amdgcn_s_memrealtime();
+  out[blockIdx.x * 3 + 0] = xcc;
+  out[blockIdx.x * 3 + 1] = t;
+  out[blockIdx.x * 3 + 2] = r;
+}
+
 }  // namespace
 }  // namespace kzgpot
 
 extern "C" {
+// 64 one-wave blocks (every XCD several times): d_out receives 64 x (xcc id, s_memtime, s_memrealtime).
+int kzgpot_synth_clock_probe(void* d_out, void* stream) {
+  hipLaunchKernelGGL(kzgpot::k_clock_probe, dim3(64), dim3(64), 0, (hipStream_t)stream, (unsigned long long*)d_out);
+  return hipGetLastError() == hipSuccess ? 0 : -101;
+}
 // Points start .. start+n-1 of stream `seed`: compressed pairing encodings into d_comp (48 / 96 B
 // each) and, if d_ark != NULL, the expected ark uncompressed bytes (96 / 192 B each). Async.
 int kzgpot_synth_g1_dev(uint64_t seed, uint64_t start, size_t n, void* d_comp, void* d_ark, void* stream) {

@@ -27,8 +27,32 @@ def synth_lib() -> ctypes.CDLL:
             fn.restype = ctypes.c_int
             fn.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p,
                            ctypes.c_void_p]
+        lib.kzgpot_synth_clock_probe.restype = ctypes.c_int
+        lib.kzgpot_synth_clock_probe.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         _synth = lib
     return _synth
+
+
+def clock_probe(device) -> torch.Tensor:
+    """Launch the clock probe on the current stream; returns its (64, 3) int64 device tensor
+    (xcc id, shader-clock counter, 100 MHz real-time counter per block)."""
+    t = torch.empty((64, 3), dtype=torch.int64, device=device)
+    if synth_lib().kzgpot_synth_clock_probe(t.data_ptr(), _stream()):
+        raise RuntimeError("kzgpot_synth_clock_probe failed")
+    return t
+
+
+def clock_mhz(before: torch.Tensor, after: torch.Tensor):
+    """Average shader clock (MHz) between two probes, per XCD (paired by XCC id: each XCD has its
+    own counters), and their mean. None if no XCD appears in both."""
+    b, a = before.cpu().tolist(), after.cpu().tolist()
+    first = {int(x): (t, r) for x, t, r in b}
+    last = {int(x): (t, r) for x, t, r in a}
+    per = {x: (last[x][0] - first[x][0]) / max(1, last[x][1] - first[x][1]) * 100.0
+           for x in sorted(first) if x in last and last[x][1] > first[x][1]}
+    if not per:
+        return None
+    return {"mean": sum(per.values()) / len(per), "per_xcd": per}
 
 
 def _stream() -> int:
