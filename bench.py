@@ -188,7 +188,7 @@ class Sharded:
         self.comp = torch.cat([p[0] for p in parts]) if len(parts) > 1 else parts[0][0]
         self.exps = [p[1] for p in parts]
         self.out = torch.empty((n if gather else self.m) * self.rout, dtype=torch.uint8, device=dev)
-        self.keys = torch.empty(len(self.blocks), dtype=torch.int64, device=dev)  # one first-bad key per launch
+        self.keys = torch.full((len(self.blocks),), -1, dtype=torch.int64, device=dev)  # one first-bad key per launch
 
     def dst(self, c):
         g0, cnt = self.blocks[c]
@@ -271,11 +271,15 @@ FALLBACKS = []  # gather-path fallbacks taken during warm-up (reported in the JS
 LAST_CLOCK = {}  # average shader clock over the last timed region (kzgpot.device.clock_mhz)
 
 
+WAIT_MS = 120_000  # warm-up: kzgpot_comm_wait's watchdog (a lost collective aborts instead of hanging)
+
+
 def lib_to_torch_gather(streams, err):
-    """Warm-up insurance for the multi-GPU run: if kzgpot_decode_allgather_dev fails, finish with
-    torch.distributed's all-gathers over the same block-cyclic layout (identical blocks when n
-    splits into world x chunks equal blocks, as every bench stream does). Returns False if a
-    stream cannot switch."""
+    """Warm-up insurance for the multi-GPU run: if kzgpot_decode_allgather_dev failed on any rank
+    in-band (every collective still issued, agreed by kzgpot.dist.agree_on_failure), EVERY rank
+    finishes with torch.distributed's all-gathers over the same block-cyclic layout (identical
+    blocks when n splits into world x chunks equal blocks, as every bench stream does). Returns
+    False if a stream cannot switch."""
     switch = [s for s in streams if s.comm is not None]
     if not switch or any(s.n % (s.world * s.chunks) for s in switch):
         return False
@@ -284,6 +288,44 @@ def lib_to_torch_gather(streams, err):
     FALLBACKS.append(f"library decode_allgather failed in warm-up ({err}); torch.distributed gathers")
     print(f"warning: {FALLBACKS[-1]}", file=sys.stderr)
     return True
+
+
+def first_warmup_step(streams, world, dev):
+    """Warm-up step 0, collective-safe: every stream is stepped even if an earlier one raised (the
+    library issues all of a call's collectives even when its decode fails, so peers stay in step),
+    library streams are completed through kzgpot_comm_wait (its status is the all-reduced key, the
+    same on every rank), and the ranks agree on ok / fallback / abort before anything else runs."""
+    import torch
+    from kzgpot import dist as KD
+
+    failed, aborted, errs = False, False, []
+    for s in streams:
+        try:
+            for w in s.step(None):
+                w.wait()
+        except RuntimeError as e:
+            failed = True
+            errs.append(str(e))
+    for s in streams:
+        if s.comm is not None:
+            rc, _ = s.comm.wait(s.keys[0:1], timeout_ms=WAIT_MS)
+            if rc in (-101, -107):  # KZGPOT_E_DEVICE / KZGPOT_E_TIMEOUT: the communicator is aborted
+                aborted = True
+                errs.append(f"kzgpot_comm_wait: {rc}")
+            elif rc == -106:  # KZGPOT_E_RANK_FAILED: some rank's decode failed, collectives complete
+                failed = True
+                errs.append("kzgpot_comm_wait: a rank failed")
+    if not aborted:
+        torch.cuda.synchronize()
+    verdict = KD.agree_on_failure(failed, aborted, dev if world > 1 and KD.dist.get_backend() == "nccl" else "cpu")
+    if verdict == "abort":
+        raise RuntimeError(f"library communicator aborted in warm-up on some rank ({'; '.join(errs) or 'peer'})")
+    if verdict == "fallback":
+        if not lib_to_torch_gather(streams, "; ".join(errs) or "a peer rank failed"):
+            raise RuntimeError(f"warm-up failed and no fallback applies ({'; '.join(errs)})")
+        for s in streams:
+            for w in s.step(None):
+                w.wait()
 
 
 def timed(streams, steps, warmup, world, dev, verify):
@@ -301,11 +343,9 @@ def timed(streams, steps, warmup, world, dev, verify):
             w.wait()  # the current stream waits for the collectives
 
     for i in range(warmup):
-        try:
-            step(None)
-        except RuntimeError as e:  # the library's decode + RCCL gather failed on this rank
-            if i or not lib_to_torch_gather(streams, e):
-                raise
+        if i == 0:
+            first_warmup_step(streams, world, dev)
+        else:
             step(None)
     torch.cuda.synchronize()
     verified = None
@@ -335,6 +375,15 @@ def timed(streams, steps, warmup, world, dev, verify):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     return elapsed, ev, verified
+
+
+def gather_label(gather_impl, args):
+    """What actually moved the blocks: the library's RCCL all-gather only when it ran (nccl backend,
+    library communicator, no warm-up fallback); otherwise torch.distributed over the backend used."""
+    if gather_impl and gather_impl.startswith("libkzgpot") and not FALLBACKS:
+        return "RCCL all-gather inside libkzgpot"
+    backend = "RCCL" if args.dist_backend == "nccl" else args.dist_backend
+    return f"torch.distributed all-gather over {backend}"
 
 
 def kernel_ms(ev, kind):
@@ -524,8 +573,8 @@ def main():
         bn_ms = kernel_ms(bn_ev, "bn254")
         next_rows["bn254_g1_decompress"] = {
             "workload": f"config 5: 2^{args.bn254_log2} BN254 G1, ark compressed 32 B -> ark uncompressed 64 B"
-                        + (f", block-cyclic shards over {world} GPUs, RCCL all-gather to one contiguous buffer "
-                           f"pipelined in {args.gather_chunks} chunks" if gather else ""),
+                        + (f", block-cyclic shards over {world} GPUs, {gather_label(gather_impl, args)} to one "
+                           f"contiguous buffer pipelined in {args.gather_chunks} chunks" if gather else ""),
             "kernel": "k_bn254_g1_decompress", "points": nb, "n_gpus": world, "steps": args.steps,
             "ms_per_step": bn_s * 1e3 / args.steps, "points_per_s": nb * args.steps / bn_s,
             "launch_ms_per_rank": bn_ms, "algorithmic_bytes_per_point": ALG_BYTES["bn254"],
@@ -634,8 +683,8 @@ def main():
             "config": {
                 "workload": f"config 4: 2^{args.g1_log2} G1 + 2^{args.g2_log2} G2 compressed BLS12-381 "
                             "points -> arkworks uncompressed, subgroup-checked"
-                            + (f", block-cyclic shards, RCCL all-gather to one contiguous buffer pipelined in "
-                               f"{args.gather_chunks} chunks" if gather else ""),
+                            + (f", block-cyclic shards, {gather_label(gather_impl, args)} to one contiguous buffer "
+                               f"pipelined in {args.gather_chunks} chunks" if gather else ""),
                 "g1_points": n1, "g2_points": n2, "parallelism": f"shard{world}",
                 "gather_impl": gather_impl if not FALLBACKS else FALLBACKS[0],
                 "subgroup_test": "endomorphism (phi/psi), bit-exact accept/reject vs ark mul_bits(r)",

@@ -46,6 +46,8 @@ extern "C" {
 #define KZGPOT_E_SIZE (-103)    /* transcript size != powersoftau CONTRIBUTION_BYTE_SIZE (preprocess-kgz.rs:83-91) */
 #define KZGPOT_E_DIGEST (-104)  /* BLAKE2b-512 mismatch (preprocess-kgz.rs:51-61, src/lib.rs:147-157) */
 #define KZGPOT_E_NETWORK (-105) /* download requested: this build has no network client */
+#define KZGPOT_E_RANK_FAILED (-106) /* multi-GPU: a rank (maybe this one) could not decode its share */
+#define KZGPOT_E_TIMEOUT (-107)     /* multi-GPU: kzgpot_comm_wait gave up; the communicator is aborted */
 
 /* ---------------------------------------------------------------- flags */
 /* Decompression only (powersoftau CheckForCorrectness::No with no read_g1 afterwards — the βτG1 /
@@ -201,7 +203,11 @@ int kzgpot_bn254_g1_decompress_dev(const void* d_in, size_t n, void* d_out, uint
  * (src/bin/preprocess-kgz.rs:105-110), whose workers fill disjoint slices of one Vec — here the
  * slices live on different GPUs and RCCL assembles them. One process (or thread) per GPU.
  *   rank 0: kzgpot_comm_unique_id(id); ship the 128 bytes to every rank (MPI, torch.distributed,
- *   a file, ...); every rank, with its GPU current: kzgpot_comm_init(&comm, id, nranks, rank). */
+ *   a file, ...); every rank, with its GPU current: kzgpot_comm_init(&comm, id, nranks, rank).
+ * RCCL is bound at first use with dlopen("librccl.so.1") (in a torch process: the RCCL torch has
+ * already loaded). KZGPOT_RCCL_LIB=<path> binds another library exporting the same symbols
+ * instead, read once per process — tests/fake_rccl is such a stand-in, running N ranks as
+ * threads of one process on one GPU. */
 #define KZGPOT_COMM_ID_BYTES 128
 int kzgpot_comm_unique_id(uint8_t* id);
 int kzgpot_comm_init(void** comm, const uint8_t* id, int nranks, int rank); /* collective */
@@ -222,9 +228,39 @@ int kzgpot_shard_layout(uint64_t n, int nranks, uint32_t chunks, uint64_t* block
  * on `stream` and then all-gathered in place (ncclAllGather on the communicator's own stream)
  * while the next chunk decodes. *d_bad_key = the first rejected point over ALL ranks as
  * (global index << 8) | status, or all ones (decode with kzgpot_decode_bad_key); rejected
- * records are zero-filled as in the single-GPU calls. `stream` waits for the gathers. */
+ * records are zero-filled as in the single-GPU calls. `stream` waits for the gathers.
+ * Collective contract: every rank calls with the same op, n, chunks and flags (the layout is
+ * derived from them). Errors never desynchronise the ranks:
+ *  - argument errors (identical on every rank, since the arguments are) return
+ *    KZGPOT_E_INVALID_ARG before any collective is queued;
+ *  - a local HIP failure (a decode launch, an event, the key buffer) stops this rank's decoding
+ *    but every collective is still issued, so no peer waits forever; the all-reduced key is then
+ *    KZGPOT_KEY_RANK_FAILED on every rank (kzgpot_comm_wait returns KZGPOT_E_RANK_FAILED) and
+ *    this call returns KZGPOT_E_DEVICE. The communicator stays usable;
+ *  - a failing RCCL call aborts the communicator (ncclCommAbort; later calls return
+ *    KZGPOT_E_DEVICE) and returns KZGPOT_E_DEVICE. Peers then fail in their own RCCL calls or
+ *    time out in kzgpot_comm_wait.
+ * Calls on one communicator are ordered: each waits (on its `stream`) for the previous call's
+ * collectives before touching the communicator's key buffers, whatever stream that call used. */
 int kzgpot_decode_allgather_dev(void* comm, int op, const void* d_in_local, uint64_t n, uint32_t chunks, void* d_out,
                                 uint32_t flags, uint64_t* d_bad_key, void* stream);
+#define KZGPOT_KEY_RANK_FAILED 0ull /* the all-reduced key when some rank failed (no real key is 0: status >= 1) */
+/* Host-side completion of kzgpot_decode_allgather_dev: waits for `stream` (polling, so that a
+ * stuck collective cannot hang the caller), then decodes *d_bad_key. Returns 0 (every point
+ * accepted), -(status) of the first rejected point (*first_bad = its global index),
+ * KZGPOT_E_RANK_FAILED when a rank could not decode its share, KZGPOT_E_DEVICE on a device or
+ * RCCL asynchronous error, or KZGPOT_E_TIMEOUT after timeout_ms (0 = no limit) — the last two
+ * abort the communicator, which makes RCCL's kernels on this rank exit (the CUDA-style watchdog
+ * a torch process group runs). first_bad may be NULL. */
+int kzgpot_comm_wait(void* comm, const uint64_t* d_bad_key, int64_t* first_bad, uint32_t timeout_ms, void* stream);
+/* Failure injection (tests and rehearsals; SURVEY §5 "failure detection"): the NEXT
+ * kzgpot_decode_allgather_dev on this communicator fails at site `site`, step `at`, once:
+ *   KZGPOT_FAULT_LAUNCH: the decode launch of chunk `at` (at == chunks: the tail) reports a HIP
+ *   launch failure; KZGPOT_FAULT_COLLECTIVE: the `at`-th all-gather (0-based; at == chunks: the
+ *   key all-reduce) reports an RCCL error. site 0 clears. */
+#define KZGPOT_FAULT_LAUNCH 1
+#define KZGPOT_FAULT_COLLECTIVE 2
+int kzgpot_comm_inject_fault(void* comm, int site, uint32_t at);
 
 /* ---------------------------------------------------------------- misc */
 const char* kzgpot_status_name(int status);  /* name of a KZGPOT_ST_* or KZGPOT_E_* code */

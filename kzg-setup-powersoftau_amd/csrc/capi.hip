@@ -757,6 +757,8 @@ const char* kzgpot_status_name(int s) {
     case KZGPOT_E_SIZE: return "SizeMismatch";
     case KZGPOT_E_DIGEST: return "DigestMismatch";
     case KZGPOT_E_NETWORK: return "NetworkUnavailable";
+    case KZGPOT_E_RANK_FAILED: return "RankFailed";
+    case KZGPOT_E_TIMEOUT: return "Timeout";
     default: return "unknown";
   }
 }

@@ -19,14 +19,24 @@
 //
 // The first rejected point over all ranks is one 8-byte ncclAllReduce(min) of the per-launch keys
 // shifted to global indices (k_merge_keys), so every rank returns the same deterministic answer.
+//
+// Failures never desynchronise the ranks (the reference's workers share one process, so it has
+// no such problem; ranks on different GPUs do). A rank whose local HIP work fails keeps issuing
+// every collective of the call — its peers receive garbage for its blocks — and all-reduces the
+// key 0 (KZGPOT_KEY_RANK_FAILED, below every real key), so every rank learns of the failure from
+// the same key. Only a failing RCCL call aborts the communicator. kzgpot_comm_wait bounds the
+// host's wait and aborts on timeout, which is what makes a peer's lost collective recoverable.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
+#include <chrono>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "codec.hpp"
@@ -38,10 +48,14 @@ namespace {
 // RCCL is bound at first use, not at link time: a process that already holds an RCCL (torch does:
 // its own librccl.so with the same SONAME) must keep using that one — a second copy loaded ahead
 // of torch corrupts the heap at exit — and single-GPU users never load it at all.
+// KZGPOT_RCCL_LIB names another library with the same symbols (tests/fake_rccl: N ranks as
+// threads on one GPU); it is opened RTLD_LOCAL so that it never interposes on torch's RCCL.
 struct Rccl {
   decltype(&ncclGetUniqueId) get_unique_id = nullptr;
   decltype(&ncclCommInitRank) comm_init_rank = nullptr;
   decltype(&ncclCommDestroy) comm_destroy = nullptr;
+  decltype(&ncclCommAbort) comm_abort = nullptr;
+  decltype(&ncclCommGetAsyncError) async_error = nullptr;  // optional
   decltype(&ncclAllGather) all_gather = nullptr;
   decltype(&ncclAllReduce) all_reduce = nullptr;
   decltype(&ncclGetErrorString) error_string = nullptr;
@@ -51,19 +65,29 @@ const Rccl& rccl() {
   static Rccl r;
   static std::once_flag once;
   std::call_once(once, [] {
-    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL | RTLD_NOLOAD);  // the process's own RCCL
-    if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    const char* over = getenv("KZGPOT_RCCL_LIB");
+    void* h = nullptr;
+    if (over && *over) {
+      h = dlopen(over, RTLD_NOW | RTLD_LOCAL);
+    } else {
+      h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL | RTLD_NOLOAD);  // the process's own RCCL
+      if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    }
     if (!h) {
-      fprintf(stderr, "kzgpot: cannot load librccl.so.1: %s\n", dlerror());
+      fprintf(stderr, "kzgpot: cannot load %s: %s\n", over && *over ? over : "librccl.so.1", dlerror());
       return;
     }
     r.get_unique_id = (decltype(r.get_unique_id))dlsym(h, "ncclGetUniqueId");
     r.comm_init_rank = (decltype(r.comm_init_rank))dlsym(h, "ncclCommInitRank");
     r.comm_destroy = (decltype(r.comm_destroy))dlsym(h, "ncclCommDestroy");
+    r.comm_abort = (decltype(r.comm_abort))dlsym(h, "ncclCommAbort");
+    r.async_error = (decltype(r.async_error))dlsym(h, "ncclCommGetAsyncError");
     r.all_gather = (decltype(r.all_gather))dlsym(h, "ncclAllGather");
     r.all_reduce = (decltype(r.all_reduce))dlsym(h, "ncclAllReduce");
     r.error_string = (decltype(r.error_string))dlsym(h, "ncclGetErrorString");
-    r.ok = r.get_unique_id && r.comm_init_rank && r.comm_destroy && r.all_gather && r.all_reduce && r.error_string;
+    r.ok = r.get_unique_id && r.comm_init_rank && r.comm_destroy && r.comm_abort && r.all_gather && r.all_reduce &&
+           r.error_string;
+    if (!r.ok) fprintf(stderr, "kzgpot: %s lacks an RCCL entry point\n", over && *over ? over : "librccl.so.1");
   });
   return r;
 }
@@ -88,12 +112,17 @@ const Rccl& rccl() {
 struct Comm {
   ncclComm_t nccl = nullptr;
   int rank = 0, nranks = 1, device = -1;
+  bool aborted = false;
   hipStream_t cs = nullptr;               // the comm stream: gathers + the key all-reduce
-  std::vector<hipEvent_t> ev;             // one per chunk (decode done) + 1 (keys merged) + 1 (all done)
+  std::vector<hipEvent_t> ev;             // one per chunk (decode done) + 1 (keys merged)
+  hipEvent_t done = nullptr;              // recorded on cs after the last collective of a call
+  bool done_recorded = false;
   unsigned long long* d_keys = nullptr;   // per-launch keys (chunks + tail)
-  uint64_t* d_local = nullptr;            // this rank's global-index min key
+  uint64_t* d_local = nullptr;            // [0] this rank's global-index min key, [1] = 0 (a failed rank's key)
   size_t cap_keys = 0;
-  std::mutex mu;                          // one call at a time per communicator (events are reused)
+  int fault_site = 0;                     // kzgpot_comm_inject_fault, one shot
+  uint32_t fault_at = 0;
+  std::mutex mu;                          // one call at a time per communicator
 };
 
 bool op_from_code(int code, CodecOp* op) {
@@ -132,6 +161,16 @@ int ensure_events(Comm& c, size_t need) {
   return 0;
 }
 
+// A failing RCCL call: the communicator cannot be trusted to line up with its peers any more.
+int abort_comm(Comm& c, ncclResult_t r, const char* what) {
+  fprintf(stderr, "kzgpot: %s failed on rank %d of %d: %s; aborting the communicator\n", what, c.rank, c.nranks,
+          r == ncclSuccess ? "timeout" : rccl().error_string(r));
+  if (c.nccl) rccl().comm_abort(c.nccl);
+  c.nccl = nullptr;
+  c.aborted = true;
+  return KZGPOT_E_DEVICE;
+}
+
 }  // namespace
 
 extern "C" {
@@ -165,7 +204,12 @@ int kzgpot_comm_init(void** comm, const uint8_t* id, int nranks, int rank) {
     return KZGPOT_E_DEVICE;
   }
   if (hipStreamCreateWithFlags(&c->cs, hipStreamNonBlocking) != hipSuccess ||
-      hipMalloc(&c->d_local, sizeof(uint64_t)) != hipSuccess) {
+      hipEventCreateWithFlags(&c->done, hipEventDisableTiming) != hipSuccess ||
+      hipMalloc(&c->d_local, 2 * sizeof(uint64_t)) != hipSuccess ||
+      hipMemset(c->d_local, 0, 2 * sizeof(uint64_t)) != hipSuccess) {
+    if (c->d_local) (void)hipFree(c->d_local);
+    if (c->done) (void)hipEventDestroy(c->done);
+    if (c->cs) (void)hipStreamDestroy(c->cs);
     rccl().comm_destroy(c->nccl);
     delete c;
     return KZGPOT_E_DEVICE;
@@ -180,12 +224,15 @@ int kzgpot_comm_destroy(void* comm) {
   int prev = -1;
   (void)hipGetDevice(&prev);
   (void)hipSetDevice(c->device);
-  (void)hipStreamSynchronize(c->cs);
+  if (!c->aborted) (void)hipStreamSynchronize(c->cs);  // an aborted comm's kernels have exited or never will
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
-  if (c->d_keys) (void)hipFree(c->d_keys);
-  if (c->d_local) (void)hipFree(c->d_local);
-  (void)hipStreamDestroy(c->cs);
-  const ncclResult_t r = rccl().comm_destroy(c->nccl);
+  (void)hipEventDestroy(c->done);
+  if (!c->aborted) {
+    if (c->d_keys) (void)hipFree(c->d_keys);
+    if (c->d_local) (void)hipFree(c->d_local);
+    (void)hipStreamDestroy(c->cs);
+  }  // else: leaked on purpose — a stuck stream may still reference them
+  const ncclResult_t r = c->nccl ? rccl().comm_destroy(c->nccl) : ncclSuccess;
   if (prev >= 0) (void)hipSetDevice(prev);
   delete c;
   return r == ncclSuccess ? 0 : KZGPOT_E_DEVICE;
@@ -198,6 +245,15 @@ int kzgpot_shard_layout(uint64_t n, int nranks, uint32_t chunks, uint64_t* block
   return 0;
 }
 
+int kzgpot_comm_inject_fault(void* comm, int site, uint32_t at) {
+  if (!comm || site < 0 || site > KZGPOT_FAULT_COLLECTIVE) return KZGPOT_E_INVALID_ARG;
+  Comm& c = *(Comm*)comm;
+  std::lock_guard<std::mutex> lock(c.mu);
+  c.fault_site = site;
+  c.fault_at = at;
+  return 0;
+}
+
 int kzgpot_decode_allgather_dev(void* comm, int op_code, const void* d_in_local, uint64_t n, uint32_t chunks,
                                 void* d_out, uint32_t flags, uint64_t* d_bad_key, void* stream) {
   CodecOp op;
@@ -205,47 +261,122 @@ int kzgpot_decode_allgather_dev(void* comm, int op_code, const void* d_in_local,
     return KZGPOT_E_INVALID_ARG;
   Comm& c = *(Comm*)comm;
   std::lock_guard<std::mutex> lock(c.mu);
+  if (c.aborted) return KZGPOT_E_DEVICE;
   int dev = -1;
   HIP_OK(hipGetDevice(&dev));
   if (dev != c.device) return KZGPOT_E_INVALID_ARG;  // the communicator's GPU must be current
   if (op == CodecOp::Bn254G1Decompress || op == CodecOp::G1Transcode || op == CodecOp::G2Transcode)
     flags &= KZGPOT_SUBGROUP_REF;
+  const int fault = c.fault_site;
+  const uint32_t fault_at = c.fault_at;
+  c.fault_site = 0;
+
+  // From here on every collective of the call is issued whatever happens locally (file comment).
   hipStream_t s = (hipStream_t)stream;
+  bool failed = false;
+  auto local = [&](hipError_t e, const char* what) {
+    if (e != hipSuccess && !failed) {
+      fprintf(stderr, "kzgpot: rank %d of %d: %s failed: %s; the gathered buffer will be incomplete\n", c.rank,
+              c.nranks, what, hipGetErrorString(e));
+      failed = true;
+    }
+    return !failed;
+  };
+  // the previous call's collectives read d_keys / d_local and used the events: wait for them
+  if (c.done_recorded) local(hipStreamWaitEvent(s, c.done, 0), "hipStreamWaitEvent(previous call)");
+  if (!failed && c.cap_keys < chunks + 1) {
+    if (c.d_keys && local(hipEventSynchronize(c.done), "hipEventSynchronize(previous call)"))
+      local(hipFree(c.d_keys), "hipFree(keys)");
+    c.d_keys = nullptr;
+    c.cap_keys = 0;
+    if (local(hipMalloc(&c.d_keys, (chunks + 1) * sizeof(unsigned long long)), "hipMalloc(keys)"))
+      c.cap_keys = chunks + 1;
+  }
+  if (!failed && ensure_events(c, chunks + 1)) local(hipErrorOutOfMemory, "hipEventCreate");
+  if (!failed) local(hipMemsetAsync(c.d_keys, 0xff, (chunks + 1) * sizeof(unsigned long long), s), "hipMemsetAsync(keys)");
+
   const uint64_t rin = in_record(op), rout = out_record(op);
   uint64_t B = 0, tail = 0;
   kzgpot_shard_layout(n, c.nranks, chunks, &B, &tail);
-  if (c.cap_keys < chunks + 1) {
-    if (c.d_keys) HIP_OK(hipFree(c.d_keys));
-    c.d_keys = nullptr;
-    c.cap_keys = 0;
-    HIP_OK(hipMalloc(&c.d_keys, (chunks + 1) * sizeof(unsigned long long)));
-    c.cap_keys = chunks + 1;
-  }
-  if (ensure_events(c, chunks + 2)) return KZGPOT_E_DEVICE;
-  HIP_OK(hipMemsetAsync(c.d_keys, 0xff, (chunks + 1) * sizeof(unsigned long long), s));
   const uint8_t* in = (const uint8_t*)d_in_local;
   uint8_t* out = (uint8_t*)d_out;
   const size_t bytes = (size_t)(B * rout);
   for (uint32_t ch = 0; B && ch < chunks; ch++) {
-    const uint64_t g0 = ((uint64_t)ch * c.nranks + c.rank) * B;
-    HIP_OK(launch_codec(op, in + ch * B * rin, out + g0 * rout, B, flags, c.d_keys + ch, nullptr, s));
-    HIP_OK(hipEventRecord(c.ev[ch], s));
-    HIP_OK(hipStreamWaitEvent(c.cs, c.ev[ch], 0));
+    if (!failed) {
+      const uint64_t g0 = ((uint64_t)ch * c.nranks + c.rank) * B;
+      const hipError_t e = fault == KZGPOT_FAULT_LAUNCH && fault_at == ch
+                               ? hipErrorLaunchFailure
+                               : launch_codec(op, in + ch * B * rin, out + g0 * rout, B, flags, c.d_keys + ch, nullptr, s);
+      if (local(e, "decode launch") && local(hipEventRecord(c.ev[ch], s), "hipEventRecord"))
+        local(hipStreamWaitEvent(c.cs, c.ev[ch], 0), "hipStreamWaitEvent");
+    }
     uint8_t* region = out + (uint64_t)ch * c.nranks * B * rout;
-    NCCL_OK(rccl().all_gather(region + (size_t)c.rank * bytes, region, bytes, ncclUint8, c.nccl, c.cs));
+    const ncclResult_t r = fault == KZGPOT_FAULT_COLLECTIVE && fault_at == ch
+                               ? ncclSystemError
+                               : rccl().all_gather(region + (size_t)c.rank * bytes, region, bytes, ncclUint8, c.nccl, c.cs);
+    if (r != ncclSuccess) return abort_comm(c, r, "ncclAllGather");
   }
-  if (tail)
-    HIP_OK(launch_codec(op, in + (uint64_t)chunks * B * rin, out + (uint64_t)chunks * c.nranks * B * rout, tail,
-                        flags, c.d_keys + chunks, nullptr, s));
-  hipLaunchKernelGGL(k_merge_keys, dim3(1), dim3(64), 0, s, c.d_keys, chunks, B, (uint32_t)c.nranks,
-                     (uint32_t)c.rank, c.d_local);
-  HIP_OK(hipGetLastError());
-  HIP_OK(hipEventRecord(c.ev[chunks], s));
-  HIP_OK(hipStreamWaitEvent(c.cs, c.ev[chunks], 0));
-  NCCL_OK(rccl().all_reduce(c.d_local, d_bad_key, 1, ncclUint64, ncclMin, c.nccl, c.cs));
-  HIP_OK(hipEventRecord(c.ev[chunks + 1], c.cs));
-  HIP_OK(hipStreamWaitEvent(s, c.ev[chunks + 1], 0));  // the caller's stream sees the whole buffer
-  return 0;
+  if (!failed && tail) {
+    const hipError_t e = fault == KZGPOT_FAULT_LAUNCH && fault_at == chunks
+                             ? hipErrorLaunchFailure
+                             : launch_codec(op, in + (uint64_t)chunks * B * rin,
+                                            out + (uint64_t)chunks * c.nranks * B * rout, tail, flags,
+                                            c.d_keys + chunks, nullptr, s);
+    local(e, "tail decode launch");
+  }
+  if (!failed) {
+    hipLaunchKernelGGL(k_merge_keys, dim3(1), dim3(64), 0, s, c.d_keys, chunks, B, (uint32_t)c.nranks,
+                       (uint32_t)c.rank, c.d_local);
+    if (local(hipGetLastError(), "key merge launch") && local(hipEventRecord(c.ev[chunks], s), "hipEventRecord"))
+      local(hipStreamWaitEvent(c.cs, c.ev[chunks], 0), "hipStreamWaitEvent");
+  }
+  // a failed rank contributes the constant 0 word (d_local[1], never written after init): the
+  // min over ranks is then KZGPOT_KEY_RANK_FAILED on every rank
+  const ncclResult_t r = fault == KZGPOT_FAULT_COLLECTIVE && fault_at == chunks
+                             ? ncclSystemError
+                             : rccl().all_reduce(failed ? c.d_local + 1 : c.d_local, d_bad_key, 1, ncclUint64,
+                                                 ncclMin, c.nccl, c.cs);
+  if (r != ncclSuccess) return abort_comm(c, r, "ncclAllReduce");
+  HIP_OK(hipEventRecord(c.done, c.cs));
+  c.done_recorded = true;
+  HIP_OK(hipStreamWaitEvent(s, c.done, 0));  // the caller's stream sees the whole buffer
+  return failed ? KZGPOT_E_DEVICE : 0;
+}
+
+int kzgpot_comm_wait(void* comm, const uint64_t* d_bad_key, int64_t* first_bad, uint32_t timeout_ms, void* stream) {
+  if (first_bad) *first_bad = -1;
+  if (!comm || !d_bad_key) return KZGPOT_E_INVALID_ARG;
+  Comm& c = *(Comm*)comm;
+  hipStream_t s = (hipStream_t)stream;
+  {
+    std::lock_guard<std::mutex> lock(c.mu);
+    if (c.aborted) return KZGPOT_E_DEVICE;
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int spin = 0;; spin++) {
+    const hipError_t q = hipStreamQuery(s);
+    if (q == hipSuccess) break;
+    if (q != hipErrorNotReady) {
+      fprintf(stderr, "kzgpot: rank %d: stream error while waiting: %s\n", c.rank, hipGetErrorString(q));
+      return KZGPOT_E_DEVICE;
+    }
+    std::lock_guard<std::mutex> lock(c.mu);
+    if (c.aborted) return KZGPOT_E_DEVICE;
+    ncclResult_t ae = ncclSuccess;
+    if (rccl().async_error && c.nccl && rccl().async_error(c.nccl, &ae) == ncclSuccess && ae != ncclSuccess &&
+        ae != ncclInProgress)
+      return abort_comm(c, ae, "asynchronous RCCL operation");
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (timeout_ms && ms > timeout_ms) {
+      abort_comm(c, ncclSuccess, "kzgpot_comm_wait");
+      return KZGPOT_E_TIMEOUT;
+    }
+    if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(200));
+  }
+  uint64_t key = ~0ull;
+  HIP_OK(hipMemcpy(&key, d_bad_key, sizeof key, hipMemcpyDeviceToHost));
+  if (key == KZGPOT_KEY_RANK_FAILED) return KZGPOT_E_RANK_FAILED;
+  return kzgpot_decode_bad_key(key, first_bad);
 }
 
 }  // extern "C"

@@ -62,6 +62,8 @@ SIGNATURES = {
     "kzgpot_comm_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "kzgpot_shard_layout": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_int, ctypes.c_uint32, u64p, u64p]),
     "kzgpot_decode_allgather_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]),
+    "kzgpot_comm_wait": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, i64p, ctypes.c_uint32, ctypes.c_void_p]),
+    "kzgpot_comm_inject_fault": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32]),
     "kzgpot_status_name": (ctypes.c_char_p, [ctypes.c_int]),
     "kzgpot_device_count": (ctypes.c_int, []),
     "kzgpot_version": (ctypes.c_char_p, []),

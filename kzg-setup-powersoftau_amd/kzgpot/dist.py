@@ -141,10 +141,40 @@ class LibComm:
         if rc:
             raise RuntimeError(f"kzgpot_decode_allgather_dev({op}) failed ({rc})")
 
+    def wait(self, key: torch.Tensor, timeout_ms: int = 0) -> tuple[int, int]:
+        """kzgpot_comm_wait on torch's current stream: (rc, first_bad). rc 0 = all accepted,
+        -(status) = a rejected point at global index first_bad, KZGPOT_E_RANK_FAILED (-106) = a
+        rank could not decode its share, KZGPOT_E_TIMEOUT (-107) / KZGPOT_E_DEVICE (-101) = the
+        communicator was aborted."""
+        fb = self._ct.c_int64(-1)
+        rc = self.lib.kzgpot_comm_wait(self.handle, key.data_ptr(), self._ct.byref(fb), timeout_ms,
+                                       torch.cuda.current_stream().cuda_stream)
+        return rc, fb.value
+
+    def inject_fault(self, site: int, at: int) -> None:
+        """Failure injection for the next decode_allgather (KZGPOT_FAULT_LAUNCH = 1 /
+        KZGPOT_FAULT_COLLECTIVE = 2; `at` = chunk or collective index)."""
+        if self.lib.kzgpot_comm_inject_fault(self.handle, site, at):
+            raise ValueError("kzgpot_comm_inject_fault: bad arguments")
+
     def close(self) -> None:
         if self.handle:
             self.lib.kzgpot_comm_destroy(self.handle)
             self.handle = self._ct.c_void_p()
+
+
+def agree_on_failure(failed: bool, aborted: bool, device, group=None) -> str:
+    """One decision every rank takes together after a library decode + gather that may have
+    failed somewhere: "ok" (no rank failed), "fallback" (some rank's decode failed in-band — the
+    library still issued every collective, so the ranks are in step and may all switch to another
+    gather path), or "abort" (some rank's communicator was aborted: collectives may be out of step,
+    nothing collective may follow on it). Deciding per rank instead would let ranks run different
+    collectives and hang."""
+    t = torch.tensor([int(bool(failed)), int(bool(aborted))], dtype=torch.int64, device=device)
+    if dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    f, a = (int(x) for x in t.tolist())
+    return "abort" if a else ("fallback" if f else "ok")
 
 
 def key_with_offset(key: int, offset: int) -> int:

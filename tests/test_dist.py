@@ -210,3 +210,42 @@ def test_bench_lib_gather_fallback():
     ragged = [mk((1 << 20) + 3, 4, 8)]
     assert not bench.lib_to_torch_gather(ragged, RuntimeError("x")) and ragged[0].comm is not None
     bench.FALLBACKS.clear()
+
+
+def _agree_worker(rank, world, port, cases, q):
+    import sys
+
+    sys.path.insert(0, os.path.join(ROOT, "kzg-setup-powersoftau_amd"))
+    from kzgpot import dist as KD
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    got = [KD.agree_on_failure(*case[rank], device="cpu") for case in cases]
+    q.put((rank, got))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_warmup_failure_decision_is_collective():
+    """bench.py's warm-up fallback: a failure injected on ONE rank must lead every
+    rank to the same decision — switch gather paths together after an in-band failure, stop
+    together after an aborted communicator — so no rank runs collectives its peers do not."""
+    world = 2
+    # per case: (failed, aborted) for rank 0, rank 1
+    cases = [((False, False), (False, False)),
+             ((False, False), (True, False)),    # rank 1's decode failed in-band
+             ((True, False), (False, False)),
+             ((False, True), (True, False)),     # rank 0's communicator aborted
+             ((False, False), (False, True))]
+    want = ["ok", "fallback", "fallback", "abort", "abort"]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_agree_worker, args=(r, world, port, cases, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(60)
+    assert res == {0: want, 1: want}

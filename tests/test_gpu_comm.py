@@ -1,11 +1,11 @@
 """The library's own multi-GPU entry (kzgpot_decode_allgather_dev: block-cyclic decode + in-place
-RCCL all-gathers + all-reduce(min) of the first bad key, include/kzgpot.h §8e). The test box has one
-GPU and RCCL refuses two ranks on one device, so this runs a one-rank communicator: every code path
-of the call (chunk loop, per-chunk events into the comm stream, the in-place ncclAllGather, the
-ragged tail, the key merge kernel and the ncclAllReduce) executes; the multi-rank exchange itself is
-the driver's 8-GPU bench (bench.py --gather-impl lib, verified by per-block checksums). Outputs are
-compared with the single-launch codec (itself parity-tested against the oracle) and the generator's
-expected bytes; bad points are planted and must come back at their global index."""
+RCCL all-gathers + all-reduce(min) of the first bad key, include/kzgpot.h §8e) with the REAL RCCL
+at one rank (RCCL refuses two ranks on one device): every code path of the call runs (chunk loop,
+per-chunk events into the comm stream, the in-place ncclAllGather, the ragged tail, the key merge
+kernel and the ncclAllReduce). The multi-rank arithmetic (rank > 0 offsets, failure paths) runs in
+tests/test_gpu_multirank.py through the test-only RCCL stand-in. Outputs are compared with the
+single-launch codec (itself parity-tested against the oracle) and the generator's expected bytes;
+bad points are planted and must come back at their global index."""
 import pytest
 
 pytestmark = pytest.mark.gpu

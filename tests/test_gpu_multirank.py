@@ -1,0 +1,106 @@
+"""The library's multi-rank decode + RCCL all-gather (kzgpot_decode_allgather_dev) at 2, 4 and 8
+ranks on one GPU: ranks are threads of one process bound to the test-only RCCL stand-in
+(tests/fake_rccl via KZGPOT_RCCL_LIB, which the library reads once per process — so the scenarios
+run in tests/multirank_driver.py, one child process, and the assertions are here).
+
+Every rank's gathered buffer must equal the generator's expected bytes, the single-launch output
+and a C-oracle re-decode of the records around every rank's block boundaries and the tail; bad
+points planted in rank 1's block and in the tail must come back at their GLOBAL index on every
+rank; an injected launch failure on one rank, and an RCCL error on one rank, must make every rank
+return non-zero without a hang. Reference anchor: src/bin/preprocess-kgz.rs:105-110 (the chunked
+parallel decompression whose disjoint slices the ranks fill here)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FAKE = os.path.join(ROOT, "tests", "fake_rccl", "build", "libfake_rccl.so")
+NO_BAD = (1 << 64) - 1
+E_DEVICE, E_RANK_FAILED, E_TIMEOUT = -101, -106, -107
+
+
+@pytest.fixture(scope="module")
+def report(gpu):
+    if not os.path.exists(FAKE):
+        subprocess.run(["make", "-C", os.path.dirname(FAKE)], check=True)
+    env = dict(os.environ, KZGPOT_RCCL_LIB=FAKE, FAKE_RCCL_TIMEOUT_S="60")
+    p = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tests", "multirank_driver.py")], env=env,
+                       capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stderr[-4000:]
+    rep = json.loads(p.stdout.strip().splitlines()[-1])
+    rep["_stderr"] = p.stderr[-6000:]  # the library's / stand-in's diagnostics, shown by failing asserts
+    if os.environ.get("GRAFT_REPO_ROOT"):  # on a gpurun box: keep the child's diagnostics with the results
+        os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+        with open(os.path.join(ROOT, "gpurun_out", "multirank_driver.err"), "w") as f:
+            f.write(p.stderr)
+    return rep
+
+
+def test_every_rank_holds_the_whole_stream(report):
+    cases = [k for k in report if "/world=" in k]
+    assert len(cases) == 8
+    for k in cases:
+        r = report[k]
+        world = int(k.rsplit("=", 1)[1])
+        assert r["hung"] == [] and r["exc"] == [None] * world, k
+        assert r["rc"] == [0] * world and r["wait"] == [0] * world, (k, r["rc"], r["wait"], report["_stderr"])
+        assert r["keys"] == [NO_BAD] * world and r["single_rank_key"] == NO_BAD, k
+        assert r["equal_expected"] == [True] * world, k
+        assert r["equal_single_rank"] == [True] * world, k
+        if r["oracle"] is not None:
+            assert r["oracle"]["equal"] and r["oracle"]["points"] > 0, k
+
+
+def test_tau_g1_ragged_layouts(report):
+    """τG1's 2^22 - 1 points in 8 chunks: tails of 15 / 31 / 63 points at 2 / 4 / 8 ranks."""
+    tails = {w: report[f"g1_decompress/n={(1 << 22) - 1}/chunks=8/world={w}"]["layout"]["tail"] for w in (2, 4, 8)}
+    assert tails == {2: 15, 4: 31, 8: 63}
+    assert report["g1_decompress/n=37/chunks=8/world=4"]["layout"] == {"block": 1, "tail": 5}
+
+
+def test_bad_point_in_rank1_block_is_global_on_every_rank(report):
+    r = report["bad_in_rank1_block"]
+    first = min(r["planted"])
+    assert r["hung"] == []
+    assert r["rc"] == [0] * 4                       # the launch succeeded everywhere
+    assert r["wait"] == [-1] * 4                    # UnexpectedCompressionMode
+    assert r["first_bad"] == [first] * 4
+    assert r["keys"] == [(first << 8) | 1] * 4
+    assert r["equal_expected_except_bad"] == [True] * 4
+
+
+def test_bad_point_in_tail_is_global_on_every_rank(report):
+    r = report["bad_in_tail"]
+    (i,) = r["planted"]
+    assert r["wait"] == [-1] * 4 and r["first_bad"] == [i] * 4
+    assert r["equal_expected_except_bad"] == [True] * 4
+
+
+def test_launch_failure_on_one_rank_fails_every_rank_without_hang(report):
+    for name, bad_rank in (("launch_failure_rank1_chunk2", 1), ("launch_failure_rank3_tail", 3)):
+        r = report[name]
+        assert r["hung"] == [], name
+        assert r["rc"] == [E_DEVICE if k == bad_rank else 0 for k in range(4)], (name, r["rc"])
+        assert r["wait"] == [E_RANK_FAILED] * 4, (name, r["wait"])
+    after = report["after_launch_failures"]         # in-band failure: the communicator stays usable
+    assert after["rc"] == [0] * 4 and after["wait"] == [0] * 4 and after["equal_expected"] == [True] * 4
+
+
+def test_collective_failure_aborts_every_rank_without_hang(report):
+    r = report["collective_failure_rank2"]
+    assert r["hung"] == []
+    assert r["rc"] == [E_DEVICE] * 4                # rank 2 aborted; its peers' RCCL calls then failed
+    assert r["seconds"] < 30
+    after = report["after_abort"]
+    assert after["rc"] == [E_DEVICE] * 4 and after["wait"] == [E_DEVICE] * 4
+
+
+def test_wait_watchdog_times_out_and_aborts(report):
+    r = report["watchdog_timeout"]
+    assert r["wait"] == E_TIMEOUT and r["seconds"] < 5
+    assert r["after"] == E_DEVICE

@@ -31,6 +31,23 @@ def test_synth_library_exports():
     assert hasattr(lib, "kzgpot_synth_g1_dev") and hasattr(lib, "kzgpot_synth_g2_dev")
 
 
+def test_fake_rccl_exports_what_the_library_binds():
+    """tests/fake_rccl stands in for librccl.so.1 in tests/test_gpu_multirank.py: it must export
+    every RCCL symbol csrc/comm.hip binds (dlsym in rccl())."""
+    path = os.path.join(ROOT, "tests", "fake_rccl", "build", "libfake_rccl.so")
+    if not os.path.exists(path):
+        subprocess.run(["make", "-C", os.path.dirname(path)], check=True)
+    src = open(os.path.join(PKG, "csrc", "comm.hip")).read()
+    import re
+
+    bound = set(re.findall(r'dlsym\(h, "(nccl[A-Za-z]+)"\)', src))
+    assert {"ncclAllGather", "ncclAllReduce", "ncclCommAbort", "ncclCommInitRank"} <= bound
+    lib = ctypes.CDLL(path)
+    assert all(hasattr(lib, s) for s in bound), bound
+    uid = ctypes.create_string_buffer(128)
+    assert lib.ncclGetUniqueId(uid) == 0 and uid.raw.startswith(b"fake_rccl:")
+
+
 def test_sizes_match_reference(kzgpot_mod):
     k = kzgpot_mod
     assert k.contribution_size(21) == 603_981_040          # preprocess-kgz.rs:83
@@ -43,6 +60,7 @@ def test_status_names(kzgpot_mod):
     k = kzgpot_mod
     assert k.status_name(-5) == "NotInSubgroup"
     assert k.status_name(-101) == "DeviceError"
+    assert k.status_name(-106) == "RankFailed" and k.status_name(-107) == "Timeout"
     assert k.status_name(0) == "ok"
     assert "gfx950" in k.version()
 
