@@ -41,7 +41,8 @@ MIX_NAMES = {"k_g1_codec": "kzgpot::k_g1_codec(",
              "k_g1_decompress": "kzgpot::k_g1_decompress(", "k_g1_check": "kzgpot::k_g1_check<(kzgpot::Src)0>",
              "k_g2_codec": "kzgpot::k_g2_codec(",
              "k_g2_decompress": "kzgpot::k_g2_decompress(", "k_g2_check": "kzgpot::k_g2_check<(kzgpot::Src)0>",
-             "k_bn254_g1_decompress": "kzgpot::k_bn254_g1_decompress("}
+             "k_bn254_g1_decompress": "kzgpot::k_bn254_g1_decompress(",
+             "k_g1_transcode": "kzgpot::k_g1_check<(kzgpot::Src)1>", "k_g2_transcode": "kzgpot::k_g2_check<(kzgpot::Src)1>"}
 RECORDS = {"g1": (48, 96, "g1_decompress"), "g2": (96, 192, "g2_decompress"),
            "bn254": (32, 64, "bn254_g1_decompress")}
 
@@ -377,6 +378,36 @@ def timed(streams, steps, warmup, world, dev, verify):
     return elapsed, ev, verified
 
 
+def transcode_row(kind, pin, out, key, want, n):
+    """SURVEY §8f row 3 (the reference's read_g1 / read_g2 loop, preprocess-kgz.rs:140-153,
+    src/lib.rs:41-80): one event-timed launch of the transcode kernel over n pairing-uncompressed
+    records (already warmed up by the caller), checked bit-exact, with its integer-VALU roof and
+    the PMC traffic per point against the algorithmic 2 x record bytes."""
+    import torch
+    from kzgpot import device as D
+    from kzgpot import dist as KD
+
+    rec = 96 if kind == "g1" else 192
+    e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    e[0].record()
+    D.codec_dev(f"{kind}_transcode", pin, out, key)
+    e[1].record()
+    torch.cuda.synchronize()
+    ms = e[0].elapsed_time(e[1])
+    pmc = load_json("pmc_traffic.json")
+    name = f"k_{kind}_transcode"
+    try:
+        traffic = pmc["kernels"][name]["bytes_per_point"]
+    except (TypeError, KeyError):
+        traffic = None
+    return {"kernel": f"k_{kind}_check<PairingBE> (read_{kind}: flags, coordinates < p, curve test, subgroup, "
+                      "ark emit)",
+            "points": n, "launch_ms": ms, "points_per_s": n / (ms * 1e-3), "ns_per_point": ms * 1e6 / n,
+            "algorithmic_bytes_per_point": 2 * rec, "pmc_bytes_per_point": traffic,
+            "valu": valu_roofline(pmc, load_json("r02_valu_mix.json"), [name], n, ms),
+            "verified_bit_exact": bool(D.read_key(key) == KD.NO_BAD and torch.equal(out, want))}
+
+
 def gather_label(gather_impl, args):
     """What actually moved the blocks: the library's RCCL all-gather only when it ran (nccl backend,
     library communicator, no warm-up fallback); otherwise torch.distributed over the backend used."""
@@ -617,16 +648,7 @@ def main():
         outt = torch.empty(nt * 96, dtype=torch.uint8, device=dev)
         keyt = torch.empty(1, dtype=torch.int64, device=dev)
         D.codec_dev("g1_transcode", pin, outt, keyt)
-        te = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-        te[0].record()
-        D.codec_dev("g1_transcode", pin, outt, keyt)
-        te[1].record()
-        torch.cuda.synchronize()
-        tr_ms = te[0].elapsed_time(te[1])
-        next_rows["g1_transcode_uncompressed"] = {
-            "kernel": "k_g1_check<PairingBE> (read_g1: flags, x/y < p, curve test, subgroup, ark emit)",
-            "points": nt, "launch_ms": tr_ms, "points_per_s": nt / (tr_ms * 1e-3), "algorithmic_bytes_per_point": 192,
-            "verified_bit_exact": bool(D.read_key(keyt) == KD.NO_BAD and torch.equal(outt, ark))}
+        next_rows["g1_transcode_uncompressed"] = transcode_row("g1", pin, outt, keyt, ark, nt)
         del pin, outt
         # 2^20 G1 + 2^20 G2 (the Fp2 square-root path) on one GPU, bit-exact
         n3 = 1 << 20
@@ -654,7 +676,15 @@ def main():
                                      n3, g2c),
             "verified_bit_exact": bool(D.read_key(k3[0:1]) == KD.NO_BAD and D.read_key(k3[1:2]) == KD.NO_BAD
                                        and torch.equal(o31, x31) and torch.equal(o32, x32))}
-        del c31, x31, c32, x32, o31, o32
+        # row 3, G2 (the read_g2 loop, the reference's HOT LOOP 2 for τG2): config 3's 2^20 ark G2
+        # records -> pairing-uncompressed (x.c1 x.c0 y.c1 y.c0, each BE) -> decoded back
+        del c31, x31, c32, o31
+        pin2 = o32.view(n3, 2, 2, 48).flip(2).flip(-1).contiguous().view(-1)
+        outt2 = torch.empty(n3 * 192, dtype=torch.uint8, device=dev)
+        keyt2 = torch.empty(1, dtype=torch.int64, device=dev)
+        D.codec_dev("g2_transcode", pin2, outt2, keyt2)
+        next_rows["g2_transcode_uncompressed"] = transcode_row("g2", pin2, outt2, keyt2, x32, n3)
+        del pin2, outt2, x32, o32
         # row 1: end-to-end preprocess (host transcript in -> host kgz / fastkzg file out, PCIe both
         # ways, BLAKE2b of both on host threads) at the reference's N = 2^21, buffers and files
         if world == 1 and args.e2e_log2 > 0:

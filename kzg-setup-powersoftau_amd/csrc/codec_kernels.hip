@@ -462,6 +462,13 @@ __global__ void __launch_bounds__(kBlock) k_g1_check(const uint4* __restrict__ i
                                                      uint64_t n, uint32_t flags,
                                                      unsigned long long* __restrict__ first_bad,
                                                      uint8_t* __restrict__ status) {
+  // The base point in Montgomery form is parked in LDS (limb-major, so the 64 lanes of a wave hit
+  // 64 consecutive dwords): each of the ~8 reloads in the ladders is 28 LDS reads instead of two
+  // Montgomery conversions, and the point costs no VGPRs between reloads. The fast test's second
+  // ladder base Q1 = [|u|]P = (X : Y : Z) is parked beside it (qpark). 70 KB per 256-lane block:
+  // 2 blocks per CU, the occupancy the VGPR count allows anyway.
+  __shared__ uint32_t base[2 * NL][kBlock];
+  __shared__ uint32_t qpark[3 * NL][kBlock];
   const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
   const uint4* rec = (src_in_place(S) ? (const uint4*)out : in) + i * 6;
@@ -469,6 +476,9 @@ __global__ void __launch_bounds__(kBlock) k_g1_check(const uint4* __restrict__ i
   int st = 0;
   bool finf;
   {
+    // The record is read ONCE: a transcode record that passes the flag and field checks is
+    // emitted right away (as k_g1_codec emits before its subgroup test) and zero-filled if the
+    // test rejects it, so nothing is re-read from HBM after the ladders (192 B/point moved).
     words x, y;
     G1Rec<S>::load_xy(x, y, rec);
     if (S == Src::ArkInPlace && x[11] == kPoison) {  // phase 1 already rejected (and reported) it
@@ -482,26 +492,24 @@ __global__ void __launch_bounds__(kBlock) k_g1_check(const uint4* __restrict__ i
     if (words_geq_p(x)) st = 3;
     else if (fpos && finf) st = 6;
     else if (words_geq_p(y)) st = 3;
-  }
-
-  if (st == 0 && !finf) {
-    // The base point in Montgomery form is parked in LDS (limb-major, so the 64 lanes of a wave
-    // hit 64 consecutive dwords): each of the ~8 reloads in the ladders is 28 LDS reads instead
-    // of two Montgomery conversions, and the point costs no VGPRs between reloads.
-    // The fast test's second ladder base Q1 = [|u|]P = (X : Y : Z) is parked beside it (qpark).
-    // 70 KB per 256-lane block: 2 blocks per CU, the occupancy the VGPR count allows anyway.
-    __shared__ uint32_t base[2 * NL][kBlock];
-    __shared__ uint32_t qpark[3 * NL][kBlock];
-    {
-      words cx, cy;
-      G1Rec<S>::load_xy(cx, cy, rec);
-      cy[11] &= 0x3fffffffu;
+    if (S != Src::ArkInPlace && st == 0) {
+      words e;
+#pragma unroll
+      for (int k = 0; k < 12; k++) e[k] = y[k];
+      if (finf) e[11] |= 0x40000000u;  // GroupAffine::new(x, y, true) keeps x, y
+      store_words(dst, x);
+      store_words(dst + 3, e);
+    }
+    if (st == 0 && !finf) {
       fp bx, by;
-      words_to_mont(bx, cx);
-      words_to_mont(by, cy);
+      words_to_mont(bx, x);
+      words_to_mont(by, y);
 #pragma unroll
       for (int k = 0; k < NL; k++) base[k][threadIdx.x] = bx.v[k], base[NL + k][threadIdx.x] = by.v[k];
     }
+  }
+
+  if (st == 0 && !finf) {
     auto load = [&](fp& bx, fp& by) {
       uint32_t lane = threadIdx.x;
       asm volatile("" : "+v"(lane));  // opaque index: re-read at every use, never hoisted
@@ -550,16 +558,7 @@ __global__ void __launch_bounds__(kBlock) k_g1_check(const uint4* __restrict__ i
     }
     if (!ok) st = 5;
   }
-  if (st) {
-    store_zero(dst, 6);
-  } else if (S != Src::ArkInPlace) {
-    words x, y;
-    G1Rec<S>::load_xy(x, y, opaque(rec));
-    y[11] &= 0x3fffffffu;
-    if (finf) y[11] |= 0x40000000u;  // GroupAffine::new(x, y, true) keeps x, y
-    store_words(dst, x);
-    store_words(dst + 3, y);
-  }
+  if (st) store_zero(dst, 6);
   report(i, st, first_bad, status);
 }
 
@@ -582,10 +581,10 @@ struct G2Rec {
 };
 
 template <Src S>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 2))) k_g2_check(const uint4* __restrict__ in, uint4* __restrict__ out,
-                                                     uint64_t n, uint32_t flags,
-                                                     unsigned long long* __restrict__ first_bad,
-                                                     uint8_t* __restrict__ status) {
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 2)))
+k_g2_check(const uint4* __restrict__ in, uint4* __restrict__ out, uint64_t n, uint32_t flags,
+           unsigned long long* __restrict__ first_bad, uint8_t* __restrict__ status) {
+  __shared__ uint32_t base[4 * NL][kBlock];  // Montgomery base point, limb-major (see k_g1_check)
   const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
   const uint4* rec = (src_in_place(S) ? (const uint4*)out : in) + i * 12;
@@ -593,6 +592,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 
   int st = 0;
   bool finf;
   {
+    // one read of the record; a transcode record is emitted before the test (see k_g1_check)
     words x0, x1, y0, y1;
     G2Rec<S>::load_xy(x0, x1, y0, y1, rec);
     if (S == Src::ArkInPlace && x0[11] == kPoison) {
@@ -607,15 +607,17 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 
     else if (words_geq_p(y0)) st = 3;
     else if (fpos && finf) st = 6;
     else if (words_geq_p(y1)) st = 3;
-  }
-
-  if (st == 0 && !finf) {
-    // Montgomery base point parked in LDS, limb-major (see k_g1_check)
-    __shared__ uint32_t base[4 * NL][kBlock];
-    {
-      words x0, x1, y0, y1;
-      G2Rec<S>::load_xy(x0, x1, y0, y1, rec);
-      y1[11] &= 0x3fffffffu;
+    if (S != Src::ArkInPlace && st == 0) {
+      store_words(dst, x0);
+      store_words(dst + 3, x1);
+      store_words(dst + 6, y0);
+      words e;
+#pragma unroll
+      for (int k = 0; k < 12; k++) e[k] = y1[k];
+      if (finf) e[11] |= 0x40000000u;
+      store_words(dst + 9, e);
+    }
+    if (st == 0 && !finf) {
       fp t;
       words_to_mont(t, x0);
 #pragma unroll
@@ -630,6 +632,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 
 #pragma unroll
       for (int k = 0; k < NL; k++) base[3 * NL + k][threadIdx.x] = t.v[k];
     }
+  }
+
+  if (st == 0 && !finf) {
     auto load = [&](fp2& bx, fp2& by) {
       uint32_t lane = threadIdx.x;
       asm volatile("" : "+v"(lane));  // opaque index: re-read at every use, never hoisted
@@ -658,18 +663,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 
       ok = in_subgroup_fast_g2(load);
     if (!ok) st = 5;
   }
-  if (st) {
-    store_zero(dst, 12);
-  } else if (S != Src::ArkInPlace) {
-    words x0, x1, y0, y1;
-    G2Rec<S>::load_xy(x0, x1, y0, y1, opaque(rec));
-    y1[11] &= 0x3fffffffu;
-    if (finf) y1[11] |= 0x40000000u;
-    store_words(dst, x0);
-    store_words(dst + 3, x1);
-    store_words(dst + 6, y0);
-    store_words(dst + 9, y1);
-  }
+  if (st) store_zero(dst, 12);
   report(i, st, first_bad, status);
 }
 

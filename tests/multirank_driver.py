@@ -122,6 +122,9 @@ class Stream:
         """Per rank: output == expected except the zero-filled records at `skip` (which must be 0)."""
         eq = []
         for o in self.outs:
+            if not skip:
+                eq.append(bool(torch.equal(o, self.exp)))
+                continue
             ov, ev = o.view(self.n, self.rout), self.exp.view(self.n, self.rout)
             keep = torch.ones(self.n, dtype=torch.bool, device=CUDA)
             if skip:
@@ -218,7 +221,19 @@ def main():
     report["after_abort"] = st.run(comms[world])
     del st
 
-    # 5. the host watchdog: kzgpot_comm_wait on a stream still busy after timeout_ms aborts the comm
+    # 5. BASELINE config 4 at its size, sharded 8 ways as the config names it: 2^27 G1 in 8 chunks
+    #    (12 GiB gathered on every rank) and 2^16 G2, every rank's whole buffer against the generator
+    torch.cuda.empty_cache()
+    for op, n, chunks in (("g1_decompress", 1 << 27, 8), ("g2_decompress", 1 << 16, 1)):
+        st = Stream(op, n, chunks, 8, seed=44)
+        r = st.run(comms[8], timeout_ms=300_000)
+        r["equal_expected"] = st.equal_expected()
+        r["layout"] = dict(zip(("block", "tail"), KD.shard_layout(n, 8, chunks)))
+        report[f"config4_full/{op}/world=8"] = r
+        del st
+        torch.cuda.empty_cache()
+
+    # 6. the host watchdog: kzgpot_comm_wait on a stream still busy after timeout_ms aborts the comm
     (c1,) = make_comms(1)
     big, _ = D.synth("g1", 3, 0, 1 << 23, CUDA, with_expected=False)
     out = torch.empty((1 << 23) * 96, dtype=torch.uint8, device=CUDA)

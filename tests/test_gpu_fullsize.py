@@ -182,3 +182,55 @@ def test_config3_g1_g2_2e20(dev, oracle_lib):
     g = kzgpot.g2_decompress(bytes(data), want_status=True)
     out, st, fb, r = oracle_run(oracle_lib, "g2_decompress", bytes(data), m, threads=16)
     assert g.status == st and g.first_bad == fb and g.ret == r and g.out == out
+
+
+def test_config5_bn254_full_size(dev):
+    """BASELINE config 5 at its size: 2^28 BN254 G1 (8 GiB in, 16 GiB out). Every point must decode
+    to the generator's expected bytes, and 32 runs of 16 records spread over the output plus its
+    last 256 records (past the 16 GiB - 16 KiB offset) are re-derived by the Python oracle (its own
+    bigint restatement of ark-bn254 0.2 deserialize -> serialize_uncompressed, independent of
+    fp381.hpp). No reference counterpart exists: BN254 is a build-defined config."""
+    torch, D = dev
+    O = pytest.importorskip("kzgpot_oracle")
+    cuda = torch.device("cuda", 0)
+    n = 1 << 28
+    comp, exp = D.synth("bn254", 28, 0, n, cuda)
+    out = torch.empty(n * 64, dtype=torch.uint8, device=cuda)
+    key = torch.empty(1, dtype=torch.int64, device=cuda)
+    D.codec_dev("bn254_g1_decompress", comp, out, key)
+    assert D.read_key(key) == (1 << 64) - 1
+    assert torch.equal(out, exp)
+    del exp
+    c, o = comp.view(-1, 32), out.view(-1, 64)
+    starts = [(k * (n // 32), 16) for k in range(32)] + [(n - 256, 256)]
+    for s, m in starts:
+        cb, ob = bytes(c[s:s + m].cpu().numpy()), bytes(o[s:s + m].cpu().numpy())
+        for j in range(m):
+            st, want = O.bn254_g1_decompress_point(cb[32 * j:32 * j + 32])
+            assert st == 0 and want == ob[64 * j:64 * j + 64], s + j
+    assert (n - 1) * 64 > 1 << 34
+
+
+def test_config4_full_size_through_library_allgather(dev):
+    """BASELINE config 4 through the multi-GPU entry point at its size: 2^27 G1 in 8 chunks and
+    2^16 G2 through kzgpot_decode_allgather_dev (the real RCCL, one rank on this one-GPU box: the
+    chunk loop, in-place gathers and key all-reduce all run; rank > 0 runs in
+    test_gpu_multirank.py). Every record must equal the generator's expected bytes."""
+    torch, D = dev
+    from kzgpot import dist as KD
+
+    cuda = torch.device("cuda", 0)
+    comm = KD.LibComm(0, 1)
+    try:
+        for kind, op, n, chunks, rout in (("g1", "g1_decompress", 1 << 27, 8, 96),
+                                         ("g2", "g2_decompress", 1 << 16, 1, 192)):
+            comp, exp = D.synth(kind, 40, 0, n, cuda)
+            out = torch.empty(n * rout, dtype=torch.uint8, device=cuda)
+            key = torch.full((1,), 0, dtype=torch.int64, device=cuda)
+            comm.decode_allgather(op, comp, n, chunks, out, key)
+            rc, fb = comm.wait(key, timeout_ms=600_000)
+            assert (rc, fb) == (0, -1), op
+            assert torch.equal(out, exp), op
+            del comp, exp, out
+    finally:
+        comm.close()

@@ -100,6 +100,16 @@ def test_collective_failure_aborts_every_rank_without_hang(report):
     assert after["rc"] == [E_DEVICE] * 4 and after["wait"] == [E_DEVICE] * 4
 
 
+def test_config4_full_size_sharded_8_ways(report):
+    """BASELINE config 4 (2^27 G1 + 2^16 G2 sharded across 8) through the library call at 8 ranks:
+    every rank ends with the whole 12 GiB (G1) / 12 MiB (G2) arkworks buffer, bit-exact."""
+    for op in ("g1_decompress", "g2_decompress"):
+        r = report[f"config4_full/{op}/world=8"]
+        assert r["hung"] == [] and r["rc"] == [0] * 8 and r["wait"] == [0] * 8, (op, r["rc"], r["wait"])
+        assert r["equal_expected"] == [True] * 8, op
+    assert report["config4_full/g1_decompress/world=8"]["layout"] == {"block": 1 << 21, "tail": 0}
+
+
 def test_wait_watchdog_times_out_and_aborts(report):
     r = report["watchdog_timeout"]
     assert r["wait"] == E_TIMEOUT and r["seconds"] < 5

@@ -37,6 +37,7 @@ KERNELS = {
     "k_g2_load": "kzgpot::k_load<4, 128>",
     "k_bn254_g1_decompress": "kzgpot::k_bn254_g1_decompress(",
     "k_g1_transcode": "kzgpot::k_g1_check<(kzgpot::Src)1>",
+    "k_g2_transcode": "kzgpot::k_g2_check<(kzgpot::Src)1>",
 }
 SIMDS_PER_XCD = 32 * 4  # GRBM_GUI_ACTIVE is summed over the 8 XCDs (one clock each); 32 CUs x 4 SIMDs per XCD
 
