@@ -640,6 +640,25 @@ def main():
             "achieved_GBs": load_gbs, "peak_GBs": HBM_PEAK_GBS, "hbm_frac": load_gbs / HBM_PEAK_GBS,
             "all_accepted": D.read_key(keyl) == KD.NO_BAD}
         del outl
+        # the same rows for G2 (load_fastkzg_setup's powers_of_h, src/lib.rs:209-215): every pair of
+        # G1 ark records read as one G2 record (x.c0 x.c1 y.c0 y.c1 = x1 y1 x2 y2: canonical
+        # coordinates, no flags), which deserialize_unchecked accepts (it checks no curve)
+        m2 = m1 // 2
+        outl = torch.empty(m2 * 200, dtype=torch.uint8, device=dev)
+        D.codec_dev("g2_load", rec1[:m2 * 192], outl, keyl)
+        le[0].record()
+        for _ in range(5):
+            D.codec_dev("g2_load", rec1[:m2 * 192], outl, keyl)
+        le[1].record()
+        torch.cuda.synchronize()
+        load2_ms = le[0].elapsed_time(le[1]) / 5
+        load2_gbs = 392 * m2 / (load2_ms * 1e-3) / 1e9
+        next_rows["g2_deserialize_unchecked"] = {
+            "kernel": "k_g2_load (load_fastkzg_setup per-point work)", "points": m2, "launch_ms": load2_ms,
+            "points_per_s": m2 / (load2_ms * 1e-3), "algorithmic_bytes_per_point": 392,
+            "achieved_GBs": load2_gbs, "peak_GBs": HBM_PEAK_GBS, "hbm_frac": load2_gbs / HBM_PEAK_GBS,
+            "all_accepted": D.read_key(keyl) == KD.NO_BAD}
+        del outl
         # row 3 (uncompressed-input mode, the read_g1 loop alone): pairing-uncompressed records =
         # per-coordinate byte reversal of the ark records (A6 identity); decode them back
         nt = min(m1, 1 << 24)

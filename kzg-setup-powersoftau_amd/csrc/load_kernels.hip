@@ -62,69 +62,91 @@ KZG_DEV void words_to_ark_mont(words& out, const words& w) {
   fp_to_words(out, x);
 }
 
-// One block handles BLK consecutive points. Records are packed at 96 / 192 B (in) and 104 / 200
+// One block handles PTS consecutive points. Records are packed at 96 / 192 B (in) and 104 / 200
 // B (out), which lane-per-record accesses would touch at a 96-200 B stride; instead the block
 // stages its whole input and output slab through LDS so that every global access is a
 // contiguous, fully coalesced 16-B-per-lane sweep.
+// A point is a lane pair: G1 one coordinate per lane (x; y with the flags), G2 two (x.c0 x.c1;
+// y.c0 y.c1 with the flags). G2 at one lane per point held 4 conversions per lane and only 3
+// waves per SIMD (LDS-bound: 200 B of slab per point): 3.8-4.0 TB/s, 5.3-5.4 as lane pairs. G1 as
+// lane pairs of 128-point blocks: 5.56 against 5.45-5.50 TB/s at one lane per point (256- or
+// 128-point blocks), same box (profiles/r03_loader_ceiling.txt) — shorter per-block compute
+// overlaps the other blocks' sweeps better.
+// The global sweeps are nontemporal (streaming: neither slab is read again by this kernel, and
+// the output is not re-read by the next): 5.54 -> 5.96 TB/s for the bare staging pattern, 5.34 ->
+// 5.51 TB/s for k_load<G1> (tools/microbench/loader_ceiling.hip, profiles/r03_loader_ceiling.txt).
 //   NC = coordinates per point (2: G1, 4: G2); the last one carries the SWFlags.
-template <int NC, int BLK>
-__global__ void __launch_bounds__(BLK) k_load(const uint4* __restrict__ in, uint4* __restrict__ out, uint64_t n,
-                                              unsigned long long* __restrict__ first_bad,
-                                              uint8_t* __restrict__ status) {
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));  // the nontemporal builtins want a vector type
+KZG_DEV uint4 ld_stream(const uint4* p) {
+  const u32x4 v = __builtin_nontemporal_load((const u32x4*)p);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+KZG_DEV void st_stream(uint4* p, const uint4& v) { __builtin_nontemporal_store((u32x4){v.x, v.y, v.z, v.w}, (u32x4*)p); }
+
+template <int NC, int PTS, bool NT = true, int CPL = 2>
+__global__ void __launch_bounds__(PTS * NC / CPL) k_load(const uint4* __restrict__ in, uint4* __restrict__ out,
+                                                         uint64_t n, unsigned long long* __restrict__ first_bad,
+                                                         uint8_t* __restrict__ status) {
+  constexpr int LPP = NC / CPL, BLK = PTS * LPP;  // lanes per point; lanes per block
   constexpr int RIN = 48 * NC, ROUT = 48 * NC + 8;
-  static_assert(RIN % 16 == 0 && (BLK * ROUT) % 16 == 0 && ROUT % 8 == 0, "slab alignment");
-  __shared__ uint4 slab[BLK * ROUT / 16];
-  const uint64_t base = (uint64_t)blockIdx.x * BLK;
-  const int cnt = (int)((n - base) < (uint64_t)BLK ? (n - base) : (uint64_t)BLK);
+  static_assert(LPP == 1 || LPP == 2, "a point is one lane or a lane pair");
+  static_assert(RIN % 16 == 0 && (PTS * ROUT) % 16 == 0 && ROUT % 8 == 0, "slab alignment");
+  __shared__ uint4 slab[PTS * ROUT / 16];
+  const uint64_t base = (uint64_t)blockIdx.x * PTS;
+  const int cnt = (int)((n - base) < (uint64_t)PTS ? (n - base) : (uint64_t)PTS);
   const int t = threadIdx.x;
+  const int pt = t / LPP, h = t % LPP;  // this lane: point pt, coordinates CPL h .. CPL h + CPL - 1
 
   const uint4* src = in + base * (RIN / 16);
   const int nin = cnt * (RIN / 16);
-  for (int k = t; k < nin; k += BLK) slab[k] = src[k];
+  for (int k = t; k < nin; k += BLK) slab[k] = NT ? ld_stream(src + k) : src[k];
   __syncthreads();
 
   int st = 0;
   bool finf = false;
-  words res[NC];
-  if (t < cnt) {
-    const uint4* rec = slab + t * (RIN / 16);
-    words c;
-    load_le(c, rec + 3 * (NC - 1));
-    const uint32_t yb = c[11] >> 24;
-    const bool fpos = yb & 0x80u;
-    finf = yb & 0x40u;
-    // ark reads the coordinates in order; the flags are parsed before the last one's range check
+  words res[CPL];
+  if (pt < cnt) {
+    // ark reads the coordinates in order, and parses the flags before the last one's range
+    // check: the lane holding the last coordinate checks its others, the flags, then the last;
+    // the first lane of a pair takes precedence (its coordinates come first).
+    const uint4* rec = slab + pt * (RIN / 16) + 3 * CPL * h;
+    const bool last = h == LPP - 1;
+    words c[CPL];
 #pragma unroll
-    for (int k = 0; k < NC - 1; k++) {
-      words a;
-      load_le(a, rec + 3 * k);
-      if (!st && words_geq_p(a)) st = 3;
-    }
-    if (!st && fpos && finf) st = 6;
-    c[11] &= 0x3fffffffu;
-    if (!st && words_geq_p(c)) st = 3;
-#pragma clang loop unroll(full)
-    for (int k = 0; k < NC; k++) {
-      words a;
-      load_le(a, rec + 3 * k);
-      if (k == NC - 1) a[11] &= 0x3fffffffu;
-      words_to_ark_mont(res[k], a);
-    }
+    for (int k = 0; k < CPL; k++) load_le(c[k], rec + 3 * k);
+    const uint32_t yb = c[CPL - 1][11] >> 24;
+    const bool fpos = yb & 0x80u;
+    finf = last && (yb & 0x40u);
+    if (last) c[CPL - 1][11] &= 0x3fffffffu;
+    if (CPL == 2 && words_geq_p(c[0])) st = 3;
+    else if (last && fpos && finf) st = 6;
+    else if (words_geq_p(c[CPL - 1])) st = 3;
+#pragma unroll
+    for (int k = 0; k < CPL; k++) words_to_ark_mont(res[k], c[k]);
+  }
+  if (LPP == 2) {  // the point's status: the first lane's, else the second's (both lanes agree)
+    const int other = __shfl_xor(st, 1);
+    st = h == 0 ? (st ? st : other) : (other ? other : st);
   }
   __syncthreads();  // every lane has read its input record: the slab becomes the output slab
-  if (t < cnt) {
-    uint2* dst = (uint2*)slab + t * (ROUT / 8);
+  if (pt < cnt) {
+    uint2* dst = (uint2*)slab + pt * (ROUT / 8) + 6 * CPL * h;
 #pragma unroll
-    for (int k = 0; k < NC; k++)
+    for (int k = 0; k < CPL; k++)
 #pragma unroll
       for (int j = 0; j < 6; j++) dst[6 * k + j] = st ? make_uint2(0, 0) : make_uint2(res[k][2 * j], res[k][2 * j + 1]);
-    dst[6 * NC] = make_uint2((!st && finf) ? 1u : 0u, 0u);
-    report(base + t, st, first_bad, status);
+    if (h == LPP - 1) {
+      dst[6 * CPL] = make_uint2((!st && finf) ? 1u : 0u, 0u);
+      report(base + pt, st, first_bad, status);
+    }
   }
   __syncthreads();
-  if (cnt == BLK) {
-    uint4* dst = (uint4*)((uint8_t*)out + base * ROUT);  // BLK * ROUT is a multiple of 16
-    for (int k = t; k < BLK * ROUT / 16; k += BLK) dst[k] = slab[k];
+  if (cnt == PTS) {
+    uint4* dst = (uint4*)((uint8_t*)out + base * ROUT);  // PTS * ROUT is a multiple of 16
+    for (int k = t; k < PTS * ROUT / 16; k += BLK) {
+      if (NT) st_stream(dst + k, slab[k]);
+      else dst[k] = slab[k];
+    }
   } else {  // ragged tail block: the slab ends on an 8-B boundary
     uint2* dst = (uint2*)out + base * (ROUT / 8);
     const uint2* s2 = (const uint2*)slab;
@@ -136,13 +158,13 @@ hipError_t launch_load(bool g2, const void* d_in, void* d_out, uint64_t n, unsig
                        uint8_t* d_status, hipStream_t stream) {
   if (n == 0) return hipSuccess;
   if (g2) {
-    constexpr int B = 128;
-    hipLaunchKernelGGL((k_load<4, B>), dim3((unsigned)((n + B - 1) / B)), dim3(B), 0, stream, (const uint4*)d_in,
+    constexpr int P = 128;  // 256 lanes, 25.6 KB of slab
+    hipLaunchKernelGGL((k_load<4, P>), dim3((unsigned)((n + P - 1) / P)), dim3(P * 2), 0, stream, (const uint4*)d_in,
                        (uint4*)d_out, n, d_first_bad, d_status);
   } else {
-    constexpr int B = 256;
-    hipLaunchKernelGGL((k_load<2, B>), dim3((unsigned)((n + B - 1) / B)), dim3(B), 0, stream, (const uint4*)d_in,
-                       (uint4*)d_out, n, d_first_bad, d_status);
+    constexpr int P = 128;  // one coordinate per lane: 256 lanes, 13.3 KB of slab
+    hipLaunchKernelGGL((k_load<2, P, true, 1>), dim3((unsigned)((n + P - 1) / P)), dim3(P * 2), 0, stream,
+                       (const uint4*)d_in, (uint4*)d_out, n, d_first_bad, d_status);
   }
   return hipGetLastError();
 }

@@ -1,0 +1,172 @@
+// Ceiling of the loader's memory pattern: k_load<G1> reads 96 B and writes
+// 104 B per point (ark bytes -> in-memory GroupAffine), staged through LDS so every global access is
+// a contiguous 16-B-per-lane sweep. How fast can that PATTERN go on this HBM, without the Fp work?
+//
+//   copy16        : plain 16-B-per-lane copy of the same input bytes (the guide's float4 copy)
+//   slab          : k_load's exact staging without the arithmetic — slab in, per-lane 96-B record
+//                   read at a 96-B LDS stride, 104-B record written back at a 104-B stride, slab out
+//   slab_nt_st    : slab with nontemporal (streaming) global stores
+//   slab_nt       : slab with nontemporal loads and stores
+//   slab_glds_nt  : slab whose input sweep is global_load_lds_dwordx4 (LDS-DMA, no VGPR round trip)
+//                   + nontemporal stores
+//   k_load        : the product kernel (kzgpot::launch_load, G1), for the same bytes
+// Every variant moves 96 + 104 B per point for 2^27 points (12.9 GB read + 14.0 GB written; copy16
+// moves 96 + 96). Reported: ms per launch (hipEvent, mean of 10 after 2 warm-ups) and TB/s of
+// algorithmic bytes.
+//
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -o bin/loader_ceiling loader_ceiling.hip
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#include "../../kzg-setup-powersoftau_amd/csrc/load_kernels.hip"
+
+#define CHECK(x)                                                                                 \
+  do {                                                                                           \
+    hipError_t e_ = (x);                                                                         \
+    if (e_ != hipSuccess) {                                                                      \
+      fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); \
+      exit(1);                                                                                   \
+    }                                                                                            \
+  } while (0)
+
+constexpr int BLK = 256;
+typedef uint32_t u4v __attribute__((ext_vector_type(4)));  // the nontemporal builtins need a vector type
+typedef __attribute__((address_space(3))) void lds_void;
+constexpr int RIN16 = 6, ROUT8 = 13, ROUT16X = 13;  // 96 B = 6 x 16; 104 B = 13 x 8
+
+__global__ void __launch_bounds__(256) k_copy16(const uint4* __restrict__ in, uint4* __restrict__ out, uint64_t n16) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n16) out[i] = in[i];
+}
+
+template <bool NT_LD, bool NT_ST, bool GLDS>
+__global__ void __launch_bounds__(BLK) k_slab(const uint4* __restrict__ in, uint4* __restrict__ out) {
+  __shared__ uint4 slab[BLK * ROUT8 / 2];
+  const int t = threadIdx.x;
+  const uint4* src = in + (uint64_t)blockIdx.x * BLK * RIN16;
+  if constexpr (GLDS) {
+    // one global_load_lds_dwordx4 per wave writes 64 x 16 B contiguously at the wave's LDS base
+    const int w = t >> 6;
+#pragma unroll
+    for (int k = 0; k < RIN16; k++) {
+      const int chunk = k * (BLK / 64) + w;  // 1 KiB chunks of the 24 KiB slab
+      __builtin_amdgcn_global_load_lds((const void*)(src + chunk * 64 + (t & 63)), (lds_void*)(slab + chunk * 64),
+                                       16, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    for (int k = t; k < BLK * RIN16; k += BLK) {
+      if (NT_LD) {
+        const u4v v = __builtin_nontemporal_load((const u4v*)(src + k));
+        slab[k] = make_uint4(v.x, v.y, v.z, v.w);
+      } else {
+        slab[k] = src[k];
+      }
+    }
+  }
+  __syncthreads();
+  uint4 r[RIN16];
+#pragma unroll
+  for (int j = 0; j < RIN16; j++) r[j] = slab[t * RIN16 + j];
+  __syncthreads();
+  uint2* d = (uint2*)slab + t * ROUT8;
+#pragma unroll
+  for (int j = 0; j < RIN16; j++) {
+    d[2 * j] = make_uint2(r[j].x ^ 1u, r[j].y);  // ^1: the bytes change, as the conversion changes them
+    d[2 * j + 1] = make_uint2(r[j].z, r[j].w);
+  }
+  d[12] = make_uint2(0, 0);
+  __syncthreads();
+  uint4* dst = out + (uint64_t)blockIdx.x * BLK * ROUT8 / 2;
+  for (int k = t; k < BLK * ROUT8 / 2; k += BLK) {
+    if (NT_ST) {
+      const uint4 v = slab[k];
+      __builtin_nontemporal_store((u4v){v.x, v.y, v.z, v.w}, (u4v*)(dst + k));
+    } else {
+      dst[k] = slab[k];
+    }
+  }
+}
+
+// random canonical ark records: every word pseudo-random, each coordinate's top word < 2^28 (value
+// < 2^380 < p, flag bits clear), so k_load converts real data (all-zero input toggles fewer bits)
+__global__ void k_fill(uint32_t* w, uint64_t nw) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= nw) return;
+  uint64_t z = (i + 1) * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  uint32_t v = (uint32_t)(z ^ (z >> 31));
+  if (i % 12 == 11) v &= 0x0fffffffu;
+  w[i] = v;
+}
+
+int main(int argc, char** argv) {
+  const int lg = argc > 1 ? atoi(argv[1]) : 27;
+  const uint64_t n = 1ull << lg;
+  uint4 *in, *out;
+  unsigned long long* key;
+  CHECK(hipMalloc(&in, n * 96));
+  CHECK(hipMalloc(&out, n * 104));
+  CHECK(hipMalloc(&key, 8));
+  const bool zero = argc > 2 && argv[2][0] == 'z';
+  if (zero) {
+    CHECK(hipMemset(in, 0, n * 96));
+  } else {
+    hipLaunchKernelGGL(k_fill, dim3((unsigned)(n * 24 / 256)), dim3(256), 0, 0, (uint32_t*)in, n * 24);
+  }
+  printf("input: %s, 2^%d points\n", zero ? "all zero" : "random canonical records", lg);
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  const double rw = (96.0 + 104.0) * n;
+  auto run = [&](const char* name, double bytes, auto launch) {
+    for (int i = 0; i < 2; i++) launch();
+    CHECK(hipDeviceSynchronize());
+    CHECK(hipEventRecord(e0));
+    for (int i = 0; i < 10; i++) launch();
+    CHECK(hipEventRecord(e1));
+    CHECK(hipEventSynchronize(e1));
+    float ms;
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    ms /= 10;
+    printf("%-16s %8.3f ms  %6.3f TB/s\n", name, ms, bytes / (ms * 1e-3) / 1e12);
+    fflush(stdout);
+  };
+  const unsigned gs = (unsigned)(n / BLK);
+  for (int rep = 0; rep < 2; rep++) {
+  printf("-- pass %d\n", rep);
+  run("copy16", 192.0 * n, [&] { hipLaunchKernelGGL(k_copy16, dim3((unsigned)(n * 6 / 256)), dim3(256), 0, 0, in, out, n * 6); });
+  run("slab", rw, [&] { hipLaunchKernelGGL((k_slab<false, false, false>), dim3(gs), dim3(BLK), 0, 0, in, out); });
+  run("slab_nt_st", rw, [&] { hipLaunchKernelGGL((k_slab<false, true, false>), dim3(gs), dim3(BLK), 0, 0, in, out); });
+  run("slab_nt", rw, [&] { hipLaunchKernelGGL((k_slab<true, true, false>), dim3(gs), dim3(BLK), 0, 0, in, out); });
+  run("slab_glds_nt", rw, [&] { hipLaunchKernelGGL((k_slab<false, true, true>), dim3(gs), dim3(BLK), 0, 0, in, out); });
+  run("k_load_plain", rw, [&] {
+    hipLaunchKernelGGL((kzgpot::k_load<2, 256, false>), dim3(gs), dim3(256), 0, 0, in, out, n, key, nullptr);
+  });
+  run("k_load (nt)", rw, [&] { CHECK(kzgpot::launch_load(false, in, out, n, key, nullptr, 0)); });
+  run("k_load 1c/l 128", rw, [&] {  // one coordinate per lane: 128 points = 256 lanes per block
+    hipLaunchKernelGGL((kzgpot::k_load<2, 128, true, 1>), dim3((unsigned)(n / 128)), dim3(256), 0, 0, in, out, n, key,
+                       nullptr);
+  });
+  run("k_load 1c/l 256", rw, [&] {  // 256 points = 512 lanes per block
+    hipLaunchKernelGGL((kzgpot::k_load<2, 256, true, 1>), dim3((unsigned)(n / 256)), dim3(512), 0, 0, in, out, n, key,
+                       nullptr);
+  });
+  run("k_load 2c/l 128", rw, [&] {  // one lane per point, 128 points per block
+    hipLaunchKernelGGL((kzgpot::k_load<2, 128, true, 2>), dim3((unsigned)(n / 128)), dim3(128), 0, 0, in, out, n, key,
+                       nullptr);
+  });
+  // G2: 192 B in + 200 B out per point, half the points
+  const uint64_t n2 = n / 2;
+  run("k_load<G2>", (192.0 + 200.0) * n2 * 1.0, [&] { CHECK(kzgpot::launch_load(true, in, out, n2, key, nullptr, 0)); });
+  run("k_load<G2>plain", (192.0 + 200.0) * n2, [&] {
+    hipLaunchKernelGGL((kzgpot::k_load<4, 128, false>), dim3((unsigned)(n2 / 128)), dim3(256), 0, 0, in, out, n2, key,
+                       nullptr);
+  });
+  }
+  CHECK(hipGetLastError());
+  return 0;
+}
