@@ -108,7 +108,14 @@ uint64_t kzgpot_contribution_size(uint32_t n_log2);
 uint64_t kzgpot_output_size(uint32_t n_log2, int mode);
 /* preprocess-{kgz,fastkgz} main (preprocess-kgz.rs:162-199, preprocess-fastkgz.rs:180-213) minus the
  * download: reads the response transcript at `transcript_path`, checks its size, decompresses and
- * checks every section on n_gpus GPUs (0 = all visible), writes `out_path`. No intermediate file.
+ * checks every section, writes `out_path`. No intermediate file.
+ * n_gpus is a SHARD count (0 = one per visible GPU; at most 64): each section is split into n_gpus contiguous
+ * shards, each driven by a host thread on GPU (current + k) mod device_count — more shards than
+ * GPUs put several shards on one GPU. The caller's current device is restored on return.
+ * File path: the transcript is pread() in 32 MiB pieces while the GPU decodes what has arrived;
+ * the output is pwrite()n as it lands into a temporary file "<out_path>.kzgpot-tmp-XXXXXX"
+ * (mkstemp: unique per call) in the same directory, renamed over out_path only on success and
+ * removed on any error, so out_path is either the complete file or untouched.
  * Returns 0 or a negative error; on a rejected point *bad_section (0 τG1, 1 τG2, 2 ατG1, 3 βτG1,
  * 4 βG2) and *bad_index locate it (pointers may be NULL). */
 int kzgpot_preprocess(const char* transcript_path, const char* out_path, int mode, uint32_t n_log2, int n_gpus,

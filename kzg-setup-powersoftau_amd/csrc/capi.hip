@@ -8,6 +8,8 @@
 
 #include <errno.h>
 #include <fcntl.h>
+#include <stdlib.h>
+#include <sys/stat.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -98,6 +100,10 @@ class Watermark {
     std::lock_guard<std::mutex> l(mu_);
     failed_ = true;
     cv_.notify_all();
+  }
+  bool failed() {
+    std::lock_guard<std::mutex> l(mu_);
+    return failed_;
   }
   // false if the reader failed before `upto` bytes arrived
   bool wait(size_t upto) {
@@ -543,15 +549,17 @@ int kzgpot_preprocess_ex(const char* transcript_path, const char* out_path, int 
     close(fd);
     return KZGPOT_E_INVALID_ARG;
   }
-  std::string tmp = std::string(out_path) + ".kzgpot-tmp-" + std::to_string((long)getpid());
-  const int ofd = open(tmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+  // unique per call (mkstemp), so concurrent calls for one out_path never share a temporary
+  std::string tmp = std::string(out_path) + ".kzgpot-tmp-XXXXXX";
+  const int ofd = mkostemp(&tmp[0], O_CLOEXEC);
   if (ofd < 0) {
     close(fd);
     return KZGPOT_E_IO;
   }
+  (void)fchmod(ofd, 0644);  // mkstemp creates 0600: a setup file is meant to be read by others
   Watermark wm;
   std::thread reader([&] {
-    for (size_t off = 0; off < len;) {
+    for (size_t off = 0; off < len && !wm.failed();) {  // stops at the next piece once the pipeline failed
       const ssize_t r = pread(fd, tr.get() + off, std::min<size_t>(len - off, (size_t)32 << 20), (off_t)off);
       if (r < 0 && errno == EINTR) continue;
       if (r <= 0) return wm.fail();
@@ -564,7 +572,7 @@ int kzgpot_preprocess_ex(const char* transcript_path, const char* out_path, int 
   io.out_fd = ofd;
   int r = preprocess_impl(tr.get(), len, out.get(), mode, n_log2, n_gpus, expect_transcript_digest,
                           transcript_digest, output_digest, bad_section, bad_index, io);
-  if (r) wm.fail();  // (the reader finishes its current pread and stops; nothing waits on it)
+  if (r) wm.fail();  // the reader finishes its current pread and stops; nothing waits on it
   reader.join();
   close(fd);
   if (close(ofd) != 0 && !r) r = KZGPOT_E_IO;

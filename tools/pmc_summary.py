@@ -67,6 +67,28 @@ def largest(dispatches):
     return {k: sum(d.get(k, 0.0) for d in ds) / len(ds) for k in keys}
 
 
+def phases(sq):
+    """VALU instructions per wave (= per point's instruction stream) of each codec phase, from the
+    SQ pass of tools/codec_phases.py: phase 1 = k_gX_decompress (flags, field checks, square
+    root(s), sign rule, emit), phase 2 = k_gX_check<ArkInPlace> (record re-read, Montgomery
+    conversion, endomorphism ladder), against the fused k_gX_codec that does both in one pass."""
+    res = {}
+    for g in ("g1", "g2"):
+        row = {}
+        for name, key in (("fused", f"k_{g}_codec"), ("phase1_decompress", f"k_{g}_decompress"),
+                          ("phase2_check", f"k_{g}_check")):
+            d = largest(sq.get(key))
+            if d and d.get("SQ_INSTS_VALU"):
+                row[name] = {"kernel": KERNELS[key], "points": int(d["_grid"]),
+                             "valu_insts_per_wave": d["SQ_INSTS_VALU"] / (d["_grid"] / 64)}
+        if {"fused", "phase1_decompress"} <= set(row):
+            f, p1 = row["fused"]["valu_insts_per_wave"], row["phase1_decompress"]["valu_insts_per_wave"]
+            row["fused_minus_phase1"] = f - p1
+            row["phase1_share_of_fused"] = p1 / f
+        res[g] = row
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("fetch")
@@ -75,6 +97,7 @@ def main():
     ap.add_argument("--out", default="profiles/pmc_traffic.json")
     ap.add_argument("--mix", default="profiles/r02_valu_mix.json")
     ap.add_argument("--source", default="rocprofv3 --pmc passes of bench.py --steps 1 --warmup 0 --no-verify")
+    ap.add_argument("--phases", help="SQ pass CSV of tools/codec_phases.py: split each codec's VALU stream by phase")
     a = ap.parse_args()
     fetch, write, sq = read(a.fetch), read(a.write), read(a.sq)
     mix = json.load(open(a.mix)) if os.path.exists(a.mix) else {"kernels": {}}
@@ -112,6 +135,8 @@ def main():
     elif "k_g1_decompress" in out["kernels"] and "k_g1_check" in out["kernels"]:
         out["g1_bytes_per_point"] = (out["kernels"]["k_g1_decompress"]["bytes_per_point"]
                                      + out["kernels"]["k_g1_check"]["bytes_per_point"])
+    if a.phases:
+        out["phases"] = phases(read(a.phases))
     with open(a.out, "w") as f:
         json.dump(out, f, indent=1)
     for k, e in out["kernels"].items():

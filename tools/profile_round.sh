@@ -21,4 +21,7 @@ timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$out/writ
   -- python3 $step > /dev/null 2> "$out/write.err"
 timeout -s KILL 180 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE \
   --output-format csv -d "$out/sq" -o run -- python3 $step > /dev/null 2> "$out/sq.err"
+# per-phase VALU split of the checked codecs (tools/codec_phases.py -> pmc_summary.py --phases)
+timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE --output-format csv -d "$out/phases" -o run \
+  -- python3 tools/codec_phases.py > "$out/codec_phases.json" 2> "$out/phases.err"
 find "$out" -name "*.csv" | sort
