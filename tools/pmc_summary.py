@@ -39,6 +39,7 @@ KERNELS = {
     "k_g1_transcode": "kzgpot::k_g1_check<(kzgpot::Src)1>",
     "k_g2_transcode": "kzgpot::k_g2_check<(kzgpot::Src)1>",
 }
+LANES_PER_POINT = {"k_g1_load": 2, "k_g2_load": 2}  # the loaders run a point as a lane pair (load_kernels.hip)
 SIMDS_PER_XCD = 32 * 4  # GRBM_GUI_ACTIVE is summed over the 8 XCDs (one clock each); 32 CUs x 4 SIMDs per XCD
 
 
@@ -111,10 +112,11 @@ def main():
         base = f or w or s
         if base is None:
             continue
-        pts = int(base["_grid"])
+        lpp = LANES_PER_POINT.get(k, 1)
+        pts = int(base["_grid"]) // lpp
         fb = 2 * 1024 * f["FETCH_SIZE"] if f and "FETCH_SIZE" in f else None
         wb = 1024 * w["WRITE_SIZE"] if w and "WRITE_SIZE" in w else None
-        e = {"points": pts, "fetch_bytes": fb, "write_bytes": wb,
+        e = {"points": pts, "lanes_per_point": lpp, "fetch_bytes": fb, "write_bytes": wb,
              "bytes_per_point": ((fb or 0) + (wb or 0)) / pts,
              "csv_vgpr": int(base["_vgpr"]), "csv_agpr": int(base["_agpr"])}
         md = next((m for name, m in mix["kernels"].items() if pat in name), None)
@@ -123,7 +125,8 @@ def main():
                       "lds_bytes_per_block": md.get("lds_bytes"), "waves_per_simd": md.get("waves_per_simd"),
                       "avg_simd_cycles_per_valu_at_roof": md.get("avg_cycles_per_valu")})
         if s and s.get("SQ_INSTS_VALU"):
-            e["valu_insts_per_wave"] = s["SQ_INSTS_VALU"] / (pts / 64)
+            e["valu_insts_per_wave"] = s["SQ_INSTS_VALU"] / (pts * lpp / 64)  # one lane's stream
+            e["valu_insts_per_point"] = e["valu_insts_per_wave"] * lpp
             if s.get("GRBM_GUI_ACTIVE"):
                 e["simd_cycles_per_valu"] = s["GRBM_GUI_ACTIVE"] * SIMDS_PER_XCD / s["SQ_INSTS_VALU"]
         for c in ("SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_ACTIVE_INST_VALU", "GRBM_GUI_ACTIVE", "SQ_WAVES"):
