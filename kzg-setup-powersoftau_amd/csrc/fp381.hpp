@@ -411,9 +411,172 @@ KZG_DEV void fp_from_mont(Fe<Tr>& canon, const Fe<Tr>& a) {
   fp_reduce_once(canon, canon);
 }
 
+// ------------------------------------------------------------------------------- radix-2^30 core
+// BLS12-381's square-root exponentiation (376 squarings + 85 multiplies per call: a third of the
+// G1 codec's instruction stream, 40 % of the G2 codec's) runs on 13 x 30-bit BALANCED limbs:
+// int32 digits in [-2^29, 2^29), R30 = 2^390, each product one v_mad_i64_i32. Signed digits keep
+// every product below 2^58 in magnitude, so the a*b and m*p column chains (13 products each) still
+// fit one 64-bit accumulator, and a multiply is 169 + 169 mads instead of 196 + 196: 75.8 against
+// 67.9 G multiplies/s, 91 against 83.6 G squarings/s (tools/microbench/mont30s.hip,
+// profiles/r03_mont30_microbench.txt). The price is headroom — an operand digit may not exceed
+// ~2^29.5 — which the ladders' lazy sums need and a pure square-and-multiply chain does not, so only
+// the exponentiation uses it. Bounds: tests/test_fp30.py (worst-case columns for the actual digits
+// of p, and an exact model of every function below against Python integers).
+constexpr int N30 = 13;
+struct f30 {
+  int32_t v[N30];
+};
+KZG_DEV int32_t sext30(uint32_t x) { return __builtin_amdgcn_sbfe((int32_t)x, 0, 30); }
+
+// r = a b 2^-390 mod p for balanced a, b (|digit| <= 2^29, top digit < 2^22); r balanced with
+// |value| < p/2 + |a| |b| / R30. The lower columns are made divisible by 2^30 by m_i = balanced
+// (col * PINV30); the upper columns start their a*b partial sum at +2^29, so that the digit
+// (acc & M30) - 2^29 and the carry acc >> 30 are the balanced remainder and its exact quotient.
+KZG_DEV void f30_mul(f30& r, const f30& a, const f30& b) {
+  constexpr int N = N30;
+  int32_t m[N];
+  int64_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < 2 * N - 1; i++) {
+    const int j0 = i < N ? 0 : i - (N - 1);
+    const int j1 = i < N ? i - 1 : N - 1;
+    int64_t accab = i < N ? 0 : (int64_t)1 << 29, accp = 0;
+#pragma unroll
+    for (int j = j0; j <= j1; j++) {
+      accab += (int64_t)a.v[j] * b.v[i - j];
+      accp += (int64_t)m[j] * P30[i - j];
+    }
+    acc += accab;
+    if (i < N) {
+      acc += (int64_t)a.v[i] * b.v[0];
+      acc += accp;
+      m[i] = sext30((uint32_t)acc * PINV30);
+      acc += (int64_t)m[i] * P30[0];
+    } else {
+      acc += accp;
+      r.v[i - N] = (int32_t)((uint32_t)acc & ((1u << 30) - 1)) - (1 << 29);
+    }
+    acc >>= 30;
+  }
+  r.v[N - 1] = (int32_t)acc;
+}
+// r = a^2 2^-390: cross products once as a_j (2 a_k), the same reduction
+KZG_DEV void f30_sqr(f30& r, const f30& a) {
+  constexpr int N = N30;
+  int32_t d[N], m[N];
+#pragma unroll
+  for (int j = 0; j < N; j++) d[j] = a.v[j] + a.v[j];
+  int64_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < 2 * N - 1; i++) {
+    const int j0 = i < N ? 0 : i - (N - 1);
+    const int k1 = i < N ? i - 1 : N - 1;
+    int64_t accab = i < N ? 0 : (int64_t)1 << 29, accp = 0;
+#pragma unroll
+    for (int j = j0; 2 * j < i; j++) accab += (int64_t)a.v[j] * d[i - j];
+    if ((i & 1) == 0) accab += (int64_t)a.v[i / 2] * a.v[i / 2];
+    acc += accab;
+#pragma unroll
+    for (int k = j0; k <= k1; k++) accp += (int64_t)m[k] * P30[i - k];
+    acc += accp;
+    if (i < N) {
+      m[i] = sext30((uint32_t)acc * PINV30);
+      acc += (int64_t)m[i] * P30[0];
+    } else {
+      r.v[i - N] = (int32_t)((uint32_t)acc & ((1u << 30) - 1)) - (1 << 29);
+    }
+    acc >>= 30;
+  }
+  r.v[N - 1] = (int32_t)acc;
+}
+// the same integer in balanced 30-bit digits; a: limbs < 2^32 - 16, value < 2^380
+KZG_DEV void f30_from_fp(f30& r, const fp& a) {
+  fp n;
+  fp_norm(n, a);
+  int32_t c = 0;
+#pragma unroll
+  for (int k = 0; k < N30; k++) {
+    const int bit = 30 * k, i = bit / 28, off = bit % 28;  // off is even and <= 24: two limbs suffice
+    uint32_t u = (n.v[i] >> off) | (i + 1 < NL ? n.v[i + 1] << (28 - off) : 0u);
+    if (k < N30 - 1) {
+      const int32_t t = (int32_t)(u & ((1u << 30) - 1)) + c;  // [0, 2^30]
+      c = (t + (1 << 29)) >> 30;
+      r.v[k] = sext30((uint32_t)t);
+    } else {
+      r.v[k] = (int32_t)u + c;
+    }
+  }
+}
+// canonical 14 x 28 limbs of a balanced value with |value| < p: + p, unsigned 30-bit digits,
+// 28-bit limbs, one conditional subtraction
+KZG_DEV void fp_from_f30(fp& r, const f30& z) {
+  uint32_t u[N30];
+  int32_t c = 0;
+#pragma unroll
+  for (int k = 0; k < N30; k++) {
+    const int32_t t = z.v[k] + P30[k] + c;
+    if (k < N30 - 1) {
+      u[k] = (uint32_t)t & ((1u << 30) - 1);
+      c = t >> 30;
+    } else {
+      u[k] = (uint32_t)t;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NL; j++) {
+    const int bit = 28 * j, i = bit / 30, off = bit % 30;
+    uint32_t v = u[i] >> off;
+    if (off > 2 && i + 1 < N30) v |= u[i + 1] << (30 - off);
+    r.v[j] = j < NL - 1 ? v & LMASK : v;
+  }
+  fp_reduce_once(r, r);
+}
+
+// BLS12-381 r = a^((p-3)/4) on the radix-2^30 core: a (R = 2^392 Montgomery) read as an R30
+// Montgomery integer is the element 4a, so the chain computes (4a)^e and one multiply by
+// POW30_OUT = 2^392 4^-e turns it into a^e in R = 2^392 Montgomery form. Same schedule and
+// register table as the generic version below. Output canonical.
+KZG_DEV void fp_pow_pm3d4_30(fp& r, const fp& a_in) {
+  typedef uint32_t v8u __attribute__((ext_vector_type(8)));
+  static_assert(BlsFp::SQRT_TABLE == 8, "table held as one 8-wide register vector per limb");
+  v8u tab[N30];
+  f30 a, a2, t;
+  f30_from_fp(a, a_in);
+  f30_sqr(a2, a);
+  t = a;
+#pragma unroll
+  for (int k = 0; k < N30; k++) tab[k][0] = (uint32_t)a.v[k];
+#pragma clang loop unroll(full)
+  for (int e = 1; e < BlsFp::SQRT_TABLE; e++) {
+    f30_mul(t, t, a2);
+#pragma unroll
+    for (int k = 0; k < N30; k++) tab[k][e] = (uint32_t)t.v[k];
+  }
+  f30 acc;
+#pragma unroll
+  for (int k = 0; k < N30; k++) acc.v[k] = (int32_t)tab[k][BlsFp::SQRT_STEP_IDX[0]];
+#pragma unroll 1
+  for (int s = 1; s < BlsFp::SQRT_STEPS; s++) {
+    const int nsq = __builtin_amdgcn_readfirstlane(BlsFp::SQRT_STEP_SQ[s]);
+    const int idx = __builtin_amdgcn_readfirstlane(BlsFp::SQRT_STEP_IDX[s]);
+#pragma unroll 1
+    for (int k = 0; k < nsq; k++) f30_sqr(acc, acc);
+    if (idx >= 0) {
+#pragma unroll
+      for (int k = 0; k < N30; k++) t.v[k] = (int32_t)tab[k][idx];
+      f30_mul(acc, acc, t);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < N30; k++) t.v[k] = POW30_OUT[k];
+  f30_mul(acc, acc, t);
+  fp_from_f30(r, acc);
+}
+
 // r = a^((p-3)/4): fixed sliding-window schedule (tools/gen_constants.py), identical for every
 // lane, so the whole wave follows one instruction stream. Loops stay rolled so one square and
-// one multiply body serve all operations (I-cache). Input limbs <= 2^30, output normalized.
+// one multiply body serve all operations (I-cache). Input limbs <= 2^30, output normalized
+// (BLS12-381: canonical, through fp_pow_pm3d4_30).
 // The 8-entry table lives in registers, one 8-wide vector per limb read with a wave-uniform
 // index (below). An earlier scratch-memory table (per-lane private memory) was cheaper in
 // instructions but its per-CU working set overflowed L2 at full occupancy: 1,479 B/point of HBM
@@ -421,6 +584,10 @@ KZG_DEV void fp_from_mont(Fe<Tr>& canon, const Fe<Tr>& a) {
 // 2,370 -> 2,343 ms per 2^27-point G1 codec pass.
 template <class Tr>
 KZG_DEV void fp_pow_pm3d4(Fe<Tr>& r, const Fe<Tr>& a) {
+  if constexpr (__is_same(Tr, BlsFp)) {
+    fp_pow_pm3d4_30(r, a);
+    return;
+  }
   static_assert(Tr::SQRT_TABLE == 8, "table held as one 8-wide register vector per limb");
   typedef uint32_t v8u __attribute__((ext_vector_type(8)));
   // tab[k][e] = limb k of a^(2e+1): a wave-uniform (SGPR) index into a register vector becomes

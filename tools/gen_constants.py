@@ -51,6 +51,24 @@ def arr(name, vals, comment=""):
     return s + (f"  // {comment}" if comment else "")
 
 
+def balanced30(x, n=13):
+    """x as n signed 30-bit digits in [-2^29, 2^29) (the last one takes the rest)."""
+    d = []
+    for k in range(n - 1):
+        r = x & ((1 << 30) - 1)
+        r -= (1 << 30) if r >= (1 << 29) else 0
+        d.append(r)
+        x = (x - r) >> 30
+    d.append(x)
+    assert -(1 << 29) <= x < (1 << 29)
+    return d
+
+
+def arr_s32(name, vals, comment=""):
+    c = f"  // {comment}" if comment else ""
+    return f"static constexpr int32_t {name}[{len(vals)}] = {{" + ", ".join(str(v) for v in vals) + "};" + c
+
+
 def mont(x):
     return x * RM % P
 
@@ -181,6 +199,7 @@ def main():
     inv2 = pow(2, P - 2, P)
     absu = -U
     bls_kb = [(c, Lb, None, None) for c, Lb in KB] + [(64, 31, None, "KB_EQ")]
+    pow30_out = (1 << 392) * pow(4, -((P - 3) // 4), P) % P
     fs, nsq, nmul = field_struct("BlsFp", P, NL, 12, bls_kb, "BLS12-381 Fq")
     lines = [
         "// GENERATED by tools/gen_constants.py — do not edit by hand.",
@@ -207,6 +226,11 @@ def main():
         arr("G2_GEN_X1", limbs28(mont(O.G2_GEN[0][1]))),
         arr("G2_GEN_Y0", limbs28(mont(O.G2_GEN[1][0]))),
         arr("G2_GEN_Y1", limbs28(mont(O.G2_GEN[1][1]))),
+        "// radix-2^30 balanced core (fp381.hpp f30_*): 13 signed limbs in [-2^29, 2^29), R30 = 2^390;",
+        "// the square-root exponentiation runs there (fp_pow_pm3d4 for BlsFp)",
+        arr_s32("P30", balanced30(P), "p, balanced 30-bit digits"),
+        f"static constexpr uint32_t PINV30 = 0x{(-pow(P, -1, 1 << 30)) % (1 << 30):08x}u;  // -p^-1 mod 2^30",
+        arr_s32("POW30_OUT", balanced30(pow30_out), "2^392 4^-e mod p, e = (p-3)/4: R30-domain (4a)^e -> R = 2^392 a^e"),
         f"static constexpr uint64_t BLS_ABS_U = 0x{absu:016x}ull;  // |u|, u < 0",
         "static constexpr int BLS_ABS_U_BITS = %d;" % absu.bit_length(),
         arr("FR_R", words32(R, 8), "group order r (ref-mode double-and-add)"),

@@ -25,10 +25,9 @@ constexpr uint32_t PINV30 = 0x3ffcfffdu;  // -p^-1 mod 2^30
 constexpr uint32_t M30 = (1u << 30) - 1;
 
 __device__ __forceinline__ int32_t sext30(uint32_t x) { return __builtin_amdgcn_sbfe((int32_t)x, 0, 30); }
-
 // r = a b 2^-390 mod p (|value| < p/2 + |a||b|/R), balanced limbs in and out. The upper
-// columns start their m*p chain at +2^29, so that limb = (acc & M30) - 2^29 and carry = acc >> 30
-// give the balanced digit and its exact quotient.
+// columns start their a*b partial sum at +2^29, so that limb = (acc & M30) - 2^29 and
+// carry = acc >> 30 give the balanced digit and its exact quotient.
 __device__ __forceinline__ void mul30(int32_t (&r)[N30], const int32_t (&a)[N30], const int32_t (&b)[N30]) {
   constexpr int N = N30;
   int32_t m[N];
@@ -37,7 +36,6 @@ __device__ __forceinline__ void mul30(int32_t (&r)[N30], const int32_t (&a)[N30]
   for (int i = 0; i < 2 * N - 1; i++) {
     const int j0 = i < N ? 0 : i - (N - 1);
     const int j1 = i < N ? i - 1 : N - 1;
-    // the bias starts the column's own a*b partial sum (first mad's addend: no extra add)
     int64_t accab = i < N ? 0 : (int64_t)1 << 29, accp = 0;
 #pragma unroll
     for (int j = j0; j <= j1; j++) {
