@@ -40,28 +40,28 @@ KZG_DEV void f_mul_sub(fp& r, const fp& a, const fp& b, const fp& c, const fp& d
 
 // ---------------------------------------------------------------- doubling
 // Hot path (G1, 126 doublings per point). In: X, Y limbs < 2^30, Z normalized, values <= 110.
-// Out: X3 limbs < 2^30 (v <= 4.1), Y3, Z3 normalized. 3S + 2M + one two-product multiply: the
-// 8C = 8B^2 term of Y3 = E (D - X3) - 8C is folded into E's product as B (-8B), so both share one
-// Montgomery reduction — 105 fewer MACs and one reduction's bookkeeping less than squaring 2B
-// separately (3S + 3M + 1S). No carry propagation except -8B's normalization.
+// Out: X3 limbs < 2^30 (v <= 4.1), Y3 limbs < 2^29 (v <= 2), Z3 normalized. 3S + 2M + one
+// multiply-plus-square: -Y3 = E (X3 - D) + 8 B^2 is ONE Montgomery reduction whose 8 B^2 half is
+// computed as a squaring (fp_mul_add8sqr: 105 mads for it where Y3 = E (D - X3) + B (-8B) took a
+// full 196-mad product and a normalized -8B), and Y3 = K - (-Y3) is a limb-wise borrowed
+// subtraction. The same field element as ark's Y3 (the reference ladder's boolean is unchanged).
 KZG_DEV void jac_dbl(jac<fp>& p) {
-  fp a, b, d, e, t, n;
+  fp a, b, d, e, t;
   fp_sqr(a, p.x);              // A = X^2                    N
   fp_sqr(b, p.y);              // B = Y^2                    N
   fp_shl_nr<2>(t, p.x);        // 4X                        < 2^32
   fp_mul(d, t, b);             // D = 4 X B                  N
-  fp_mul3_nr(e, a);            // E = 3A                    < 3 * 2^28
+  fp_mul3_nr(e, a);
+  fp_norm(e, e);               // E = 3A                     N (v <= 3.01)
   fp_shl_nr<1>(t, p.y);        // 2Y                        < 2^31
   fp_mul(p.z, t, p.z);         // Z3 = 2 Y Z                 N
   fp_sqr(a, e);                // F = E^2                    N
   fp_shl_nr<1>(t, d);          // 2D                        < 2^29
   fp_subk_nr(p.x, a, t, BlsFp::KB_8_29);  // X3 = F - 2D           < 2^30 + 2^28
-  fp_mul3_nr(t, d);            // 3D
-  fp_subk_nr(t, t, a, BlsFp::KB_8_28);    // D - X3 = 3D - F       < 5 * 2^28
-  fp_shl_nr<3>(n, b);          // 8B                        < 2^31
-  fp_negk_nr(n, n, BlsFp::KB_64_31);      // -8B                   < 2^32
-  fp_norm(n, n);               //                            N (v <= 64)
-  fp_mul_sum2(p.y, e, t, b, n);  // Y3 = E (D - X3) + B (-8B)  N
+  fp_mul3_nr(t, d);            // 3D                        < 3 * 2^28
+  fp_subk_nr(t, a, t, BlsFp::KB_8_30);    // X3 - D = F - 3D       < 2^30 + 2^28
+  fp_mul_add8sqr(d, e, t, b);  // -Y3 = E (X3 - D) + 8 B^2   N
+  fp_negk_nr(p.y, d, BlsFp::KB_2_28);     // Y3                    < 2^29
 }
 
 // ---------------------------------------------------------------- Fp2, carry-free (G2 ladders)

@@ -141,6 +141,25 @@ def mul_sum3(a: V, b: V, c: V, d: V, e: V, f: V, name="mul_sum3"):
     return normalized(((a.val * b.val + c.val * d.val + e.val * f.val) * P_OVER_R + 1) * UP, name)
 
 
+def mul_add8sqr(a: V, b: V, c: V, name="mul_add8sqr"):
+    """fp_mul_add8sqr: a b + 8 c^2 with one reduction; the c^2 half as a squaring (cross products
+    c_j (16 c_k) once, squares c_j (8 c_j)), whose column sums equal those of c (8 c)."""
+    if max(c.limbs) << 4 >= 1 << 32:
+        raise BoundError(f"{name}: 16 c_k must fit 32 bits ({c!r})")
+    c8 = V([x << 3 for x in c.limbs], c.val * 8 * UP, name + ".8c")
+    carry = 0
+    for i in range(2 * NL):
+        j0 = 0 if i < NL else i - (NL - 1)
+        j1 = i if i < NL else NL - 1
+        s = sum(a.limbs[j] * b.limbs[i - j] + c.limbs[j] * c8.limbs[i - j] for j in range(j0, j1 + 1))
+        s += sum(LM * P_L[i - j] for j in range(j0, j1 + 1))
+        s += carry
+        if s >= 1 << 64:
+            raise BoundError(f"{name}: column {i} may reach {s.bit_length()} bits")
+        carry = s >> LB
+    return normalized(((a.val * b.val + 8 * c.val * c.val) * P_OVER_R + 1) * UP, name)
+
+
 def sqr(a: V, name="sqr"):
     """fp_sqr: same column sums as mul(a, a); the doubled operand 2 a_k must fit 32 bits."""
     if max(a.limbs) >= 1 << 31:
@@ -307,21 +326,20 @@ class Field:
 # ------------------------------------------------------------------------------------------
 # formulas (mirror csrc/curve.hpp)
 def jac_dbl_fp(X, Y, Z):
-    """jac_dbl(jac<fp>&) — the hot path (Y3 = E (D - X3) + B (-8B) in one reduction)."""
+    """jac_dbl(jac<fp>&) — the hot path (-Y3 = E (X3 - D) + 8 B^2 in one reduction, Y3 = K - that)."""
     a = sqr(X, "A")
     b = sqr(Y, "B")
     t = shl(X, 2)
     d = mul(t, b, "D")
-    e = mul3(a)
+    e = norm(mul3(a), "E")
     t = shl(Y, 1)
     z3 = mul(t, Z, "Z3")
     f = sqr(e, "F")
     t = shl(d, 1)
     x3 = subk(f, t, "KB_8_29", "X3")
-    t = mul3(d)
-    t = subk(t, f, "KB_8_28", "3D-F")
-    n = norm(subk(normalized(0), shl(b, 3), "KB_64_31", "-8B"), "-8B")
-    y3 = mul_sum2(e, t, b, n, "Y3")
+    t = subk(f, mul3(d), "KB_8_30", "F-3D")
+    ny3 = mul_add8sqr(e, t, b, "-Y3")
+    y3 = subk(normalized(0), ny3, "KB_2_28", "Y3")
     return x3, y3, z3
 
 
