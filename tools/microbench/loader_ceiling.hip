@@ -10,6 +10,10 @@
 //   slab_glds_nt  : slab whose input sweep is global_load_lds_dwordx4 (LDS-DMA, no VGPR round trip)
 //                   + nontemporal stores
 //   k_load        : the product kernel (kzgpot::launch_load, G1), for the same bytes
+//   k_load_pipe   : an experiment: a resident grid (x f/4 of the occupancy-limited block count)
+//                   walks the slabs grid-stride, prefetching the next slab's input into registers
+//                   while it converts and stores the current one. Slower than letting the hardware
+//                   keep ~8 independent blocks per CU in flight (4.9 vs 5.55 TB/s)
 // Every variant moves 96 + 104 B per point for 2^27 points (12.9 GB read + 14.0 GB written; copy16
 // moves 96 + 96). Reported: ms per launch (hipEvent, mean of 10 after 2 warm-ups) and TB/s of
 // algorithmic bytes.
@@ -21,6 +25,98 @@
 #include <stdlib.h>
 
 #include "../../kzg-setup-powersoftau_amd/csrc/load_kernels.hip"
+
+// The same per-point work as k_load, software-pipelined: a grid of resident blocks walks the
+// slabs grid-stride, and each block issues the NEXT slab's input loads (into registers, PER per
+// lane) before it converts and stores the current one, so the input latency hides behind the
+// block's own compute and store sweep instead of only behind other blocks'.
+namespace kzgpot {
+// EXPERIMENT (not in the product; measured slower, profiles/r03_loader_ceiling.txt):
+template <int NC, int PTS, int CPL = 2>
+__global__ void __launch_bounds__(PTS * NC / CPL) k_load_pipe(const uint4* __restrict__ in, uint4* __restrict__ out,
+                                                              uint64_t n, unsigned long long* __restrict__ first_bad,
+                                                              uint8_t* __restrict__ status) {
+  constexpr int LPP = NC / CPL, BLK = PTS * LPP;
+  constexpr int RIN = 48 * NC, ROUT = 48 * NC + 8;
+  constexpr int NIN16 = PTS * RIN / 16, PER = (NIN16 + BLK - 1) / BLK;
+  static_assert(LPP == 1 || LPP == 2, "a point is one lane or a lane pair");
+  static_assert(RIN % 16 == 0 && (PTS * ROUT) % 16 == 0 && ROUT % 8 == 0, "slab alignment");
+  __shared__ uint4 slab[PTS * ROUT / 16];
+  const uint64_t nslabs = (n + PTS - 1) / PTS;
+  const int t = threadIdx.x;
+  const int pt = t / LPP, h = t % LPP;
+  uint4 pre[PER];
+  auto fetch = [&](uint64_t sl) {
+    const uint64_t b = sl * PTS;
+    const int c = (int)((n - b) < (uint64_t)PTS ? (n - b) : (uint64_t)PTS);
+    const uint4* src = in + b * (RIN / 16);
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+      const int k = t + q * BLK;
+      if (k < c * (RIN / 16)) pre[q] = ld_stream(src + k);
+    }
+  };
+  uint64_t sl = blockIdx.x;
+  if (sl < nslabs) fetch(sl);
+  for (; sl < nslabs; sl += gridDim.x) {
+    const uint64_t base = sl * PTS;
+    const int cnt = (int)((n - base) < (uint64_t)PTS ? (n - base) : (uint64_t)PTS);
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+      const int k = t + q * BLK;
+      if (k < cnt * (RIN / 16)) slab[k] = pre[q];
+    }
+    __syncthreads();
+    if (sl + gridDim.x < nslabs) fetch(sl + gridDim.x);  // in flight during the work below
+
+    int st = 0;
+    bool finf = false;
+    words res[CPL];
+    if (pt < cnt) {
+      const uint4* rec = slab + pt * (RIN / 16) + 3 * CPL * h;
+      const bool last = h == LPP - 1;
+      words c[CPL];
+#pragma unroll
+      for (int k = 0; k < CPL; k++) load_le(c[k], rec + 3 * k);
+      const uint32_t yb = c[CPL - 1][11] >> 24;
+      const bool fpos = yb & 0x80u;
+      finf = last && (yb & 0x40u);
+      if (last) c[CPL - 1][11] &= 0x3fffffffu;
+      if (CPL == 2 && words_geq_p(c[0])) st = 3;
+      else if (last && fpos && finf) st = 6;
+      else if (words_geq_p(c[CPL - 1])) st = 3;
+#pragma unroll
+      for (int k = 0; k < CPL; k++) words_to_ark_mont(res[k], c[k]);
+    }
+    if (LPP == 2) {
+      const int other = __shfl_xor(st, 1);
+      st = h == 0 ? (st ? st : other) : (other ? other : st);
+    }
+    __syncthreads();
+    if (pt < cnt) {
+      uint2* dst = (uint2*)slab + pt * (ROUT / 8) + 6 * CPL * h;
+#pragma unroll
+      for (int k = 0; k < CPL; k++)
+#pragma unroll
+        for (int j = 0; j < 6; j++) dst[6 * k + j] = st ? make_uint2(0, 0) : make_uint2(res[k][2 * j], res[k][2 * j + 1]);
+      if (h == LPP - 1) {
+        dst[6 * CPL] = make_uint2((!st && finf) ? 1u : 0u, 0u);
+        report(base + pt, st, first_bad, status);
+      }
+    }
+    __syncthreads();
+    if (cnt == PTS) {
+      uint4* dst = (uint4*)((uint8_t*)out + base * ROUT);
+      for (int k = t; k < PTS * ROUT / 16; k += BLK) st_stream(dst + k, slab[k]);
+    } else {
+      uint2* dst = (uint2*)out + base * (ROUT / 8);
+      const uint2* s2 = (const uint2*)slab;
+      for (int k = t; k < cnt * (ROUT / 8); k += BLK) dst[k] = s2[k];
+    }
+    __syncthreads();  // the slab is read out before the next slab's input overwrites it
+  }
+}
+}  // namespace kzgpot
 
 #define CHECK(x)                                                                                 \
   do {                                                                                           \
@@ -159,8 +255,31 @@ int main(int argc, char** argv) {
     hipLaunchKernelGGL((kzgpot::k_load<2, 128, true, 2>), dim3((unsigned)(n / 128)), dim3(128), 0, 0, in, out, n, key,
                        nullptr);
   });
+  // software-pipelined loader (k_load_pipe): a resident grid walks the slabs grid-stride and
+  // prefetches the next slab's input while it converts and stores the current one
+  int cus = 0, occ1 = 0, occ2 = 0;
+  CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+  CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ1, kzgpot::k_load_pipe<2, 128, 1>, 256, 0));
+  CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ2, kzgpot::k_load_pipe<4, 128, 2>, 256, 0));
+  if (rep == 0) printf("k_load_pipe: %d CUs, %d / %d resident blocks per CU (G1 / G2)\n", cus, occ1, occ2);
+  for (int f = 1; f <= 4; f *= 2) {
+    char nm[32];
+    snprintf(nm, sizeof nm, "k_load_pipe x%d/4", f);
+    const unsigned g = (unsigned)(cus * occ1 * f / 4);
+    run(nm, rw, [&] {
+      hipLaunchKernelGGL((kzgpot::k_load_pipe<2, 128, 1>), dim3(g), dim3(256), 0, 0, in, out, n, key, nullptr);
+    });
+  }
   // G2: 192 B in + 200 B out per point, half the points
   const uint64_t n2 = n / 2;
+  for (int f = 2; f <= 4; f *= 2) {
+    char nm[32];
+    snprintf(nm, sizeof nm, "k_load_pipe<G2> x%d/4", f);
+    const unsigned g = (unsigned)(cus * occ2 * f / 4);
+    run(nm, (192.0 + 200.0) * n2, [&] {
+      hipLaunchKernelGGL((kzgpot::k_load_pipe<4, 128, 2>), dim3(g), dim3(256), 0, 0, in, out, n2, key, nullptr);
+    });
+  }
   run("k_load<G2>", (192.0 + 200.0) * n2 * 1.0, [&] { CHECK(kzgpot::launch_load(true, in, out, n2, key, nullptr, 0)); });
   run("k_load<G2>plain", (192.0 + 200.0) * n2, [&] {
     hipLaunchKernelGGL((kzgpot::k_load<4, 128, false>), dim3((unsigned)(n2 / 128)), dim3(256), 0, 0, in, out, n2, key,
