@@ -226,8 +226,7 @@ KZG_DEV void jac_madd(jac<F>& p, Load&& load) {
   }
   F hh, j;
   f_sqr(hh, h);                // HH
-  f_shl<1>(t, p.z);
-  f_norm(t, t);
+  f_shl<1>(t, p.z);            // 2 Z1 (Z is a product: normalized, so 2 Z1 < 2^29 needs no carry)
   f_mul(p.z, t, h);            // Z3 = 2 Z1 H  (= (Z1 + H)^2 - Z1Z1 - HH)
   f_shl<2>(hh, hh);
   f_norm(hh, hh);              // I = 4 HH
@@ -241,10 +240,8 @@ KZG_DEV void jac_madd(jac<F>& p, Load&& load) {
   f_norm(t, t);                // X3 = r^2 - J - 2V
   f_subk(hh, hh, t, BlsFp::KB_128_28);
   f_norm(hh, hh);              // V - X3
-  f_shl<1>(r, r);
-  f_norm(r, r);                // r = 2 r'
-  f_shl<1>(h, p.y);
-  f_norm(h, h);                // 2 Y1
+  f_shl<1>(r, r);              // r = 2 r'     < 2^29
+  f_shl<1>(h, p.y);            // 2 Y1         < 2^30
   f_mul_sub(p.y, r, hh, h, j); // Y3 = r (V - X3) - 2 Y1 J
   p.x = t;
 }

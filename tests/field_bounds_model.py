@@ -357,7 +357,7 @@ def jac_madd(F, X, Y, Z, x2, y2):
     F.canon_ok(Z), F.canon_ok(h), F.canon_ok(r)
     xd, yd, zd = jac_dbl(F, X, Y, Z)  # the equal-point branch
     hh = F.sqr(h, "HH")
-    t = F.norm(F.shl(Z, 1))
+    t = F.shl(Z, 1)
     z3 = F.mul(t, h, "Z3")
     hh = F.norm(F.shl(hh, 2))
     j = F.mul(h, hh, "J")
@@ -368,8 +368,8 @@ def jac_madd(F, X, Y, Z, x2, y2):
     h2 = F.shl(hh, 1)
     t = F.norm(F.subk(t, h2, "KB_64_29", "X3"))
     hh = F.norm(F.subk(hh, t, "KB_128_28", "V-X3"))
-    r = F.norm(F.shl(r, 1))
-    h = F.norm(F.shl(Y, 1))
+    r = F.shl(r, 1)
+    h = F.shl(Y, 1)
     y3 = F.mul_sub(r, hh, h, j, "Y3")  # r (V - X3) - 2 Y1 J
     one = F.one()
     jn = (lambda a, b: V2(vmax(a.c0, b.c0), vmax(a.c1, b.c1))) if F.two else vmax
