@@ -28,13 +28,14 @@ struct jac {
 // Fp forms used by the generic jac_madd / jac_eq_affine (instantiated for Fp; the G2 ladders
 // have their own carry-free Fp2 overloads below): carry-free limb-wise forms, bounds proven by
 // tests/test_field_bounds.py.
-KZG_DEV void f_subk(fp& r, const fp& a, const fp& b, const uint32_t (&k)[NL]) { fp_subk_nr(r, a, b, k); }
+template <const auto& K>
+KZG_DEV void f_subk(fp& r, const fp& a, const fp& b) { fp_subk_nr<K>(r, a, b); }
 template <int S>
 KZG_DEV void f_shl(fp& r, const fp& a) { fp_shl_nr<S>(r, a); }
 // r = a b - c d in one reduction (d negated as a borrowed multiple of p)
 KZG_DEV void f_mul_sub(fp& r, const fp& a, const fp& b, const fp& c, const fp& d) {
   fp nd;
-  fp_negk_nr(nd, d, BlsFp::KB_4_28);
+  fp_negk_nr<BlsFp::KB_4_28>(nd, d);
   fp_mul_sum2(r, a, b, c, nd);
 }
 
@@ -45,7 +46,9 @@ KZG_DEV void f_mul_sub(fp& r, const fp& a, const fp& b, const fp& c, const fp& d
 // computed as a squaring (fp_mul_add8sqr: 105 mads for it where Y3 = E (D - X3) + B (-8B) took a
 // full 196-mad product and a normalized -8B), and Y3 = K - (-Y3) is a limb-wise borrowed
 // subtraction. The same field element as ark's Y3 (the reference ladder's boolean is unchanged).
-KZG_DEV void jac_dbl(jac<fp>& p) {
+// z_one (wave-uniform): Z is the Montgomery 1 (a ladder's first step from its affine base), so
+// Z3 = 2 Y Z is 2Y: a carry pass instead of a multiply.
+KZG_DEV void jac_dbl(jac<fp>& p, bool z_one = false) {
   fp a, b, d, e, t;
   fp_sqr(a, p.x);              // A = X^2                    N
   fp_sqr(b, p.y);              // B = Y^2                    N
@@ -54,14 +57,17 @@ KZG_DEV void jac_dbl(jac<fp>& p) {
   fp_mul3_nr(e, a);
   fp_norm(e, e);               // E = 3A                     N (v <= 3.01)
   fp_shl_nr<1>(t, p.y);        // 2Y                        < 2^31
-  fp_mul(p.z, t, p.z);         // Z3 = 2 Y Z                 N
+  if (__builtin_expect(z_one, 0))
+    fp_norm(p.z, t);           // Z3 = 2 Y                   N
+  else
+    fp_mul(p.z, t, p.z);       // Z3 = 2 Y Z                 N
   fp_sqr(a, e);                // F = E^2                    N
   fp_shl_nr<1>(t, d);          // 2D                        < 2^29
-  fp_subk_nr(p.x, a, t, BlsFp::KB_8_29);  // X3 = F - 2D           < 2^30 + 2^28
+  fp_subk_nr<BlsFp::KB_8_29>(p.x, a, t);  // X3 = F - 2D           < 2^30 + 2^28
   fp_mul3_nr(t, d);            // 3D                        < 3 * 2^28
-  fp_subk_nr(t, a, t, BlsFp::KB_8_30);    // X3 - D = F - 3D       < 2^30 + 2^28
+  fp_subk_nr<BlsFp::KB_8_30>(t, a, t);    // X3 - D = F - 3D       < 2^30 + 2^28
   fp_mul_add8sqr(d, e, t, b);  // -Y3 = E (X3 - D) + 8 B^2   N
-  fp_negk_nr(p.y, d, BlsFp::KB_2_28);     // Y3                    < 2^29
+  fp_negk_nr<BlsFp::KB_2_28>(p.y, d);     // Y3                    < 2^29
 }
 
 // ---------------------------------------------------------------- Fp2, carry-free (G2 ladders)
@@ -72,25 +78,28 @@ KZG_DEV void jac_dbl(jac<fp>& p) {
 // jac_madd_fp2_lz, jac_eq_affine_fp2_lz) proves for all inputs; ladder states stay normalized
 // with values below ~21 p.
 // r = a b with b.c1 negated against k (k must dominate b.c1): two Montgomery reductions
-KZG_DEV void f2_mul_lz(fp2& r, const fp2& a, const fp2& b, const uint32_t (&k)[NL]) {
+template <const auto& K>
+KZG_DEV void f2_mul_lz(fp2& r, const fp2& a, const fp2& b) {
   fp nb1, c0;
-  fp_negk_nr(nb1, b.c1, k);
+  fp_negk_nr<K>(nb1, b.c1);
   fp_mul_sum2(c0, a.c0, b.c0, a.c1, nb1);
   fp_mul_sum2(r.c1, a.c0, b.c1, a.c1, b.c0);
   r.c0 = c0;
 }
 // r = a^2 = (a0 + a1)(a0 - a1) + 2 a0 a1 u, the difference against k (dominating a.c1)
-KZG_DEV void f2_sqr_lz(fp2& r, const fp2& a, const uint32_t (&k)[NL]) {
+template <const auto& K>
+KZG_DEV void f2_sqr_lz(fp2& r, const fp2& a) {
   fp s, d, t;
   fp_add_nr(s, a.c0, a.c1);
-  fp_subk_nr(d, a.c0, a.c1, k);
+  fp_subk_nr<K>(d, a.c0, a.c1);
   fp_shl_nr<1>(t, a.c0);
   fp_mul(r.c1, t, a.c1);
   fp_mul(r.c0, s, d);
 }
-KZG_DEV void f2_subk(fp2& r, const fp2& a, const fp2& b, const uint32_t (&k)[NL]) {
-  fp_subk_nr(r.c0, a.c0, b.c0, k);
-  fp_subk_nr(r.c1, a.c1, b.c1, k);
+template <const auto& K>
+KZG_DEV void f2_subk(fp2& r, const fp2& a, const fp2& b) {
+  fp_subk_nr<K>(r.c0, a.c0, b.c0);
+  fp_subk_nr<K>(r.c1, a.c1, b.c1);
 }
 template <int S>
 KZG_DEV void f2_shl(fp2& r, const fp2& a) {
@@ -110,31 +119,31 @@ KZG_DEV void f2_norm(fp2& r, const fp2& a) {
 // MACs and 2 reductions where C's squaring plus E (D - X3) took 1,960 and 4.
 KZG_DEV void jac_dbl(jac<fp2>& p) {
   fp2 b, a, d, t;
-  f2_sqr_lz(b, p.y, BlsFp::KB_32_28);        // B = Y^2
+  f2_sqr_lz<BlsFp::KB_32_28>(b, p.y);        // B = Y^2
   f2_shl<1>(t, p.y);
-  f2_mul_lz(p.z, t, p.z, BlsFp::KB_16_28);   // Z3 = 2 Y Z          (Y dead)
-  f2_sqr_lz(a, p.x, BlsFp::KB_16_28);        // A = X^2
+  f2_mul_lz<BlsFp::KB_16_28>(p.z, t, p.z);   // Z3 = 2 Y Z          (Y dead)
+  f2_sqr_lz<BlsFp::KB_16_28>(a, p.x);        // A = X^2
   f2_shl<2>(t, p.x);
-  f2_mul_lz(d, t, b, BlsFp::KB_2_28);        // D = 4 X B           (X dead)
+  f2_mul_lz<BlsFp::KB_2_28>(d, t, b);        // D = 4 X B           (X dead)
   fp_mul3_nr(a.c0, a.c0);
   fp_mul3_nr(a.c1, a.c1);
   f2_norm(a, a);                             // E = 3 A             (A dead)
-  f2_sqr_lz(t, a, BlsFp::KB_4_28);           // F = E^2
+  f2_sqr_lz<BlsFp::KB_4_28>(t, a);           // F = E^2
   f2_shl<1>(p.x, d);
-  f2_subk(p.x, t, p.x, BlsFp::KB_4_29);
+  f2_subk<BlsFp::KB_4_29>(p.x, t, p.x);
   f2_norm(p.x, p.x);                         // X3 = F - 2D         (F dead)
-  f2_subk(d, d, p.x, BlsFp::KB_8_28);        // t = D - X3
+  f2_subk<BlsFp::KB_8_28>(d, d, p.x);        // t = D - X3
   fp u, s, n, c0;
-  fp_negk_nr(u, d.c1, BlsFp::KB_16_30);      // -t1
+  fp_negk_nr<BlsFp::KB_16_30>(u, d.c1);      // -t1
   fp_add_nr(s, b.c0, b.c1);                  // b0 + b1             < 2^29
-  fp_subk_nr(n, b.c0, b.c1, BlsFp::KB_2_28);
+  fp_subk_nr<BlsFp::KB_2_28>(n, b.c0, b.c1);
   fp_norm(n, n);                             // b0 - b1             N
   fp_shl_nr<3>(n, n);
-  fp_negk_nr(n, n, BlsFp::KB_64_31);
+  fp_negk_nr<BlsFp::KB_64_31>(n, n);
   fp_norm(n, n);                             // -8 (b0 - b1)        N
   fp_mul_sum3(c0, a.c0, d.c0, a.c1, u, s, n);
   fp_shl_nr<3>(n, b.c1);
-  fp_negk_nr(n, n, BlsFp::KB_16_31);
+  fp_negk_nr<BlsFp::KB_16_31>(n, n);
   fp_norm(n, n);                             // -8 b1               N
   fp_shl_nr<1>(s, b.c0);                     // 2 b0                < 2^29
   fp_mul_sum3(p.y.c1, a.c0, d.c1, a.c1, d.c0, s, n);
@@ -149,13 +158,13 @@ KZG_DEV void jac_madd(jac<fp2>& p, Load&& load) {
   {
     fp2 x2, y2;
     load(x2, y2);
-    f2_sqr_lz(z1z1, p.z, BlsFp::KB_2_28);
-    f2_mul_lz(h, x2, z1z1, BlsFp::KB_2_28);  // U2
-    f2_subk(h, h, p.x, BlsFp::KB_32_28);
+    f2_sqr_lz<BlsFp::KB_2_28>(z1z1, p.z);
+    f2_mul_lz<BlsFp::KB_2_28>(h, x2, z1z1);  // U2
+    f2_subk<BlsFp::KB_32_28>(h, h, p.x);
     f2_norm(h, h);                           // H = U2 - X1
-    f2_mul_lz(t, y2, p.z, BlsFp::KB_2_28);
-    f2_mul_lz(t, t, z1z1, BlsFp::KB_2_28);   // S2
-    f2_subk(r, t, p.y, BlsFp::KB_32_28);
+    f2_mul_lz<BlsFp::KB_2_28>(t, y2, p.z);
+    f2_mul_lz<BlsFp::KB_2_28>(t, t, z1z1);   // S2
+    f2_subk<BlsFp::KB_32_28>(r, t, p.y);
     f2_norm(r, r);                           // r' = S2 - Y1   (ark's r = 2 r')
   }
   const bool z1zero = f_is_zero(p.z);
@@ -170,24 +179,24 @@ KZG_DEV void jac_madd(jac<fp2>& p, Load&& load) {
     return;
   }
   fp2 hh, j;
-  f2_sqr_lz(hh, h, BlsFp::KB_64_28);         // HH
+  f2_sqr_lz<BlsFp::KB_64_28>(hh, h);         // HH
   f2_shl<1>(t, p.z);
-  f2_mul_lz(p.z, t, h, BlsFp::KB_64_28);     // Z3 = 2 Z1 H
+  f2_mul_lz<BlsFp::KB_64_28>(p.z, t, h);     // Z3 = 2 Z1 H
   f2_shl<2>(hh, hh);                         // I = 4 HH
-  f2_mul_lz(j, h, hh, BlsFp::KB_8_30);       // J = H I
-  f2_mul_lz(hh, p.x, hh, BlsFp::KB_8_30);    // V = X1 I
-  f2_sqr_lz(t, r, BlsFp::KB_64_28);          // r'^2
+  f2_mul_lz<BlsFp::KB_8_30>(j, h, hh);       // J = H I
+  f2_mul_lz<BlsFp::KB_8_30>(hh, p.x, hh);    // V = X1 I
+  f2_sqr_lz<BlsFp::KB_64_28>(t, r);          // r'^2
   f2_shl<2>(t, t);                           // r^2 = 4 r'^2
-  f2_subk(t, t, j, BlsFp::KB_2_28);
+  f2_subk<BlsFp::KB_2_28>(t, t, j);
   f2_shl<1>(h, hh);                          // 2V
-  f2_subk(t, t, h, BlsFp::KB_4_29);
+  f2_subk<BlsFp::KB_4_29>(t, t, h);
   f2_norm(t, t);                             // X3 = r^2 - J - 2V
-  f2_subk(hh, hh, t, BlsFp::KB_32_28);       // V - X3
+  f2_subk<BlsFp::KB_32_28>(hh, hh, t);       // V - X3
   f2_shl<1>(r, r);                           // r = 2 r'
-  f2_mul_lz(hh, r, hh, BlsFp::KB_64_30);     // r (V - X3)
+  f2_mul_lz<BlsFp::KB_64_30>(hh, r, hh);     // r (V - X3)
   f2_shl<1>(h, p.y);                         // 2 Y1
-  f2_mul_lz(j, h, j, BlsFp::KB_2_28);        // 2 Y1 J
-  f2_subk(p.y, hh, j, BlsFp::KB_4_28);
+  f2_mul_lz<BlsFp::KB_2_28>(j, h, j);        // 2 Y1 J
+  f2_subk<BlsFp::KB_4_28>(p.y, hh, j);
   f2_norm(p.y, p.y);                         // Y3 = r (V - X3) - 2 Y1 J
   p.x = t;
 }
@@ -206,11 +215,11 @@ KZG_DEV void jac_madd(jac<F>& p, Load&& load) {
     load(x2, y2);
     f_sqr(z1z1, p.z);
     f_mul(h, x2, z1z1);        // U2
-    f_subk(h, h, p.x, BlsFp::KB_128_31);
+    f_subk<BlsFp::KB_128_31>(h, h, p.x);
     f_norm(h, h);              // H = U2 - X1
     f_mul(t, y2, p.z);
     f_mul(t, t, z1z1);         // S2
-    f_subk(r, t, p.y, BlsFp::KB_64_31);
+    f_subk<BlsFp::KB_64_31>(r, t, p.y);
     f_norm(r, r);              // r' = S2 - Y1   (ark's r = 2 r')
   }
   const bool z1zero = f_is_zero(p.z);
@@ -234,11 +243,11 @@ KZG_DEV void jac_madd(jac<F>& p, Load&& load) {
   f_mul(hh, p.x, hh);          // V = X1 I
   f_sqr(t, r);                 // r'^2
   f_shl<2>(t, t);              // r^2 = 4 r'^2
-  f_subk(t, t, j, BlsFp::KB_32_28);
+  f_subk<BlsFp::KB_32_28>(t, t, j);
   f_shl<1>(h, hh);             // 2V
-  f_subk(t, t, h, BlsFp::KB_64_29);
+  f_subk<BlsFp::KB_64_29>(t, t, h);
   f_norm(t, t);                // X3 = r^2 - J - 2V
-  f_subk(hh, hh, t, BlsFp::KB_128_28);
+  f_subk<BlsFp::KB_128_28>(hh, hh, t);
   f_norm(hh, hh);              // V - X3
   f_shl<1>(r, r);              // r = 2 r'     < 2^29
   f_shl<1>(h, p.y);            // 2 Y1         < 2^30
@@ -247,13 +256,18 @@ KZG_DEV void jac_madd(jac<F>& p, Load&& load) {
 }
 
 // [|u|] B for the affine finite base B delivered by load(x, y): 63 doublings, 5 mixed additions.
+// G1: the first doubling starts from Z = 1 (jac_dbl's z_one: no Z multiply). G2 keeps the multiply:
+// 2Y may reach 2.02 p, past what the mixed addition's borrowed constants dominate.
 template <typename F, typename Load>
 KZG_DEV void mul_abs_u_affine(jac<F>& acc, Load&& load) {
   load(acc.x, acc.y);
   f_one(acc.z);
 #pragma unroll 1
   for (int b = BLS_ABS_U_BITS - 2; b >= 0; b--) {
-    jac_dbl(acc);
+    if constexpr (__is_same(F, fp))
+      jac_dbl(acc, b == BLS_ABS_U_BITS - 2);
+    else
+      jac_dbl(acc);
     if ((BLS_ABS_U >> b) & 1) jac_madd(acc, load);
   }
 }
@@ -263,11 +277,11 @@ KZG_DEV bool jac_eq_affine(const jac<F>& p, const F& x, const F& y) {
   F z2, t;
   f_sqr(z2, p.z);
   f_mul(t, x, z2);
-  f_subk(t, t, p.x, BlsFp::KB_128_31);
+  f_subk<BlsFp::KB_128_31>(t, t, p.x);
   bool ok = f_is_zero(t);
   f_mul(z2, z2, p.z);
   f_mul(t, y, z2);
-  f_subk(t, t, p.y, BlsFp::KB_128_31);
+  f_subk<BlsFp::KB_128_31>(t, t, p.y);
   ok = ok && f_is_zero(t);
   return ok && !f_is_zero(p.z);
 }
@@ -275,13 +289,13 @@ KZG_DEV bool jac_eq_affine(const jac<F>& p, const F& x, const F& y) {
 // The same test on a carry-free G2 ladder state; x, y reduced or normalized with value < 1.01 p.
 KZG_DEV bool jac_eq_affine(const jac<fp2>& p, const fp2& x, const fp2& y) {
   fp2 z2, t;
-  f2_sqr_lz(z2, p.z, BlsFp::KB_2_28);
-  f2_mul_lz(t, x, z2, BlsFp::KB_2_28);
-  f2_subk(t, t, p.x, BlsFp::KB_32_28);
+  f2_sqr_lz<BlsFp::KB_2_28>(z2, p.z);
+  f2_mul_lz<BlsFp::KB_2_28>(t, x, z2);
+  f2_subk<BlsFp::KB_32_28>(t, t, p.x);
   bool ok = f_is_zero(t);
-  f2_mul_lz(z2, z2, p.z, BlsFp::KB_2_28);
-  f2_mul_lz(t, y, z2, BlsFp::KB_2_28);
-  f2_subk(t, t, p.y, BlsFp::KB_32_28);
+  f2_mul_lz<BlsFp::KB_2_28>(z2, z2, p.z);
+  f2_mul_lz<BlsFp::KB_2_28>(t, y, z2);
+  f2_subk<BlsFp::KB_32_28>(t, t, p.y);
   ok = ok && f_is_zero(t);
   return ok && !f_is_zero(p.z);
 }

@@ -27,6 +27,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <utility>
+
 #include "bls12_381_consts.hpp"
 #include "bn254_consts.hpp"
 
@@ -247,17 +249,33 @@ KZG_DEV void fp_mul3_nr(Fe<Tr>& r, const Fe<Tr>& a) {
 #pragma unroll
   for (int i = 0; i < Tr::NL; i++) r.v[i] = (a.v[i] << 1) + a.v[i];
 }
+// K - b with the constant K in the instruction: a VOP2 v_sub_u32 with a literal. Written so because
+// the compiler otherwise hoists the borrowed constants into SGPRs, and the codecs' SGPR budget is
+// spent: every use then reloads a spilled SGPR with a v_readlane (a VALU instruction plus hazard
+// wait states) inside the ladders.
+template <uint32_t C>
+KZG_DEV uint32_t lit_sub(uint32_t b) {
+  uint32_t r;
+  asm("v_sub_u32_e32 %0, %1, %2" : "=v"(r) : "n"(C), "v"(b));
+  return r;
+}
+template <const auto& K, class Tr, size_t... I>
+KZG_DEV void subk_lit(Fe<Tr>& r, const Fe<Tr>& a, const Fe<Tr>& b, std::index_sequence<I...>) {
+  ((r.v[I] = a.v[I] + lit_sub<K[I]>(b.v[I])), ...);
+}
+template <const auto& K, class Tr, size_t... I>
+KZG_DEV void negk_lit(Fe<Tr>& r, const Fe<Tr>& b, std::index_sequence<I...>) {
+  ((r.v[I] = lit_sub<K[I]>(b.v[I])), ...);
+}
 // r = a + K - b with K a borrowed multiple of p dominating b limb by limb
-template <class Tr>
-KZG_DEV void fp_subk_nr(Fe<Tr>& r, const Fe<Tr>& a, const Fe<Tr>& b, const uint32_t (&k)[Tr::NL]) {
-#pragma unroll
-  for (int i = 0; i < Tr::NL; i++) r.v[i] = (a.v[i] + k[i]) - b.v[i];
+template <const auto& K, class Tr>
+KZG_DEV void fp_subk_nr(Fe<Tr>& r, const Fe<Tr>& a, const Fe<Tr>& b) {
+  subk_lit<K>(r, a, b, std::make_index_sequence<Tr::NL>{});
 }
 // r = K - b (the additive inverse of b, as a borrowed multiple K of p minus b, limb by limb)
-template <class Tr>
-KZG_DEV void fp_negk_nr(Fe<Tr>& r, const Fe<Tr>& b, const uint32_t (&k)[Tr::NL]) {
-#pragma unroll
-  for (int i = 0; i < Tr::NL; i++) r.v[i] = k[i] - b.v[i];
+template <const auto& K, class Tr>
+KZG_DEV void fp_negk_nr(Fe<Tr>& r, const Fe<Tr>& b) {
+  negk_lit<K>(r, b, std::make_index_sequence<Tr::NL>{});
 }
 // carry-propagate to 28-bit limbs (value unchanged; top limb keeps the excess)
 template <class Tr>
@@ -359,7 +377,7 @@ KZG_DEV bool fp_is_zero(const Fe<Tr>& a) {
 template <class Tr>
 KZG_DEV bool fp_eq(const Fe<Tr>& a, const Fe<Tr>& b) {
   Fe<Tr> d;
-  fp_subk_nr(d, a, b, Tr::KB_EQ);
+  fp_subk_nr<Tr::KB_EQ>(d, a, b);
   return fp_is_zero(d);
 }
 // canonical a < canonical b
@@ -391,7 +409,7 @@ KZG_DEV void fp_add(Fe<Tr>& r, const Fe<Tr>& a, const Fe<Tr>& b) {
 // a - b for b with limbs < 2^31 - 8 and value < 63 p (BLS12-381)
 KZG_DEV void fp_sub(fp& r, const fp& a, const fp& b) {
   fp t;
-  fp_subk_nr(t, a, b, BlsFp::KB_64_31);
+  fp_subk_nr<BlsFp::KB_64_31>(t, a, b);
   fp_norm(r, t);
 }
 KZG_DEV void fp_neg(fp& r, const fp& a) {
@@ -715,7 +733,7 @@ KZG_DEV void f_norm(fp& r, const fp& a) { fp_norm(r, a); }
 KZG_DEV void f_mul(fp2& r, const fp2& a, const fp2& b) {
   fp nb1, zero, c0;
   fp_zero(zero);
-  fp_subk_nr(nb1, zero, b.c1, BlsFp::KB_4_28);  // 4p - b1, limbs < 2^29
+  fp_subk_nr<BlsFp::KB_4_28>(nb1, zero, b.c1);  // 4p - b1, limbs < 2^29
   fp_mul_sum2(c0, a.c0, b.c0, a.c1, nb1);
   fp_mul_sum2(r.c1, a.c0, b.c1, a.c1, b.c0);
   r.c0 = c0;
@@ -724,7 +742,7 @@ KZG_DEV void f_mul(fp2& r, const fp2& a, const fp2& b) {
 KZG_DEV void f_sqr(fp2& r, const fp2& a) {
   fp s, d, t;
   fp_add_nr(s, a.c0, a.c1);
-  fp_subk_nr(d, a.c0, a.c1, BlsFp::KB_4_28);
+  fp_subk_nr<BlsFp::KB_4_28>(d, a.c0, a.c1);
   fp_shl_nr<1>(t, a.c0);
   fp_mul(r.c1, t, a.c1);
   fp_mul(r.c0, s, d);

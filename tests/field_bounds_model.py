@@ -416,16 +416,21 @@ def ladder_invariant(F, base_x, base_y, rounds=12):
     """A bound set S for the ladder accumulator (X, Y, Z) that contains the starting point and is
     CLOSED under one ladder step (dbl, then optionally madd(base)) — hence bounds every state
     reached by mul_abs_u_affine / in_subgroup_ref for any input. Found by joined iteration, then
-    inflated and verified closed."""
+    inflated and verified closed. For G1 the set also contains mul_abs_u_affine's first step, whose
+    doubling starts from Z = 1 and sets Z3 = norm(2Y) without a multiply (jac_dbl z_one)."""
     X, Y, Z = base_x, base_y, F.one()
 
-    def step(X, Y, Z):
+    def step(X, Y, Z, z_one=False):
         x1, y1, z1 = jac_dbl(F, X, Y, Z)
+        if z_one and not F.two:
+            z1 = norm(shl(Y, 1), "Z3=2Y")
         outs = [(x1, y1, z1), jac_madd(F, x1, y1, z1, base_x, base_y)]
         nx, ny, nz = X, Y, Z
         for ox, oy, oz in outs:
             nx, ny, nz = join(F, nx, ox), join(F, ny, oy), join(F, nz, oz)
         return nx, ny, nz
+
+    X, Y, Z = step(X, Y, Z, z_one=not F.two)
 
     for _ in range(rounds):
         X, Y, Z = step(X, Y, Z)
