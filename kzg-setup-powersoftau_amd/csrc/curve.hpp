@@ -46,9 +46,7 @@ KZG_DEV void f_mul_sub(fp& r, const fp& a, const fp& b, const fp& c, const fp& d
 // computed as a squaring (fp_mul_add8sqr: 105 mads for it where Y3 = E (D - X3) + B (-8B) took a
 // full 196-mad product and a normalized -8B), and Y3 = K - (-Y3) is a limb-wise borrowed
 // subtraction. The same field element as ark's Y3 (the reference ladder's boolean is unchanged).
-// z_one (wave-uniform): Z is the Montgomery 1 (a ladder's first step from its affine base), so
-// Z3 = 2 Y Z is 2Y: a carry pass instead of a multiply.
-KZG_DEV void jac_dbl(jac<fp>& p, bool z_one = false) {
+KZG_DEV void jac_dbl(jac<fp>& p) {
   fp a, b, d, e, t;
   fp_sqr(a, p.x);              // A = X^2                    N
   fp_sqr(b, p.y);              // B = Y^2                    N
@@ -57,10 +55,7 @@ KZG_DEV void jac_dbl(jac<fp>& p, bool z_one = false) {
   fp_mul3_nr(e, a);
   fp_norm(e, e);               // E = 3A                     N (v <= 3.01)
   fp_shl_nr<1>(t, p.y);        // 2Y                        < 2^31
-  if (__builtin_expect(z_one, 0))
-    fp_norm(p.z, t);           // Z3 = 2 Y                   N
-  else
-    fp_mul(p.z, t, p.z);       // Z3 = 2 Y Z                 N
+  fp_mul(p.z, t, p.z);         // Z3 = 2 Y Z                 N
   fp_sqr(a, e);                // F = E^2                    N
   fp_shl_nr<1>(t, d);          // 2D                        < 2^29
   fp_subk_nr<BlsFp::KB_8_29>(p.x, a, t);  // X3 = F - 2D           < 2^30 + 2^28
@@ -68,6 +63,57 @@ KZG_DEV void jac_dbl(jac<fp>& p, bool z_one = false) {
   fp_subk_nr<BlsFp::KB_8_30>(t, a, t);    // X3 - D = F - 3D       < 2^30 + 2^28
   fp_mul_add8sqr(d, e, t, b);  // -Y3 = E (X3 - D) + 8 B^2   N
   fp_negk_nr<BlsFp::KB_2_28>(p.y, d);     // Y3                    < 2^29
+}
+
+// 3P from the affine base (x, y) (Z = 1): EFD tpl-2007-bl with Z1 = 1 —
+//   XX = x^2, YY = y^2, YYYY = YY^2, M = 3 XX, E = 6 ((x + YY)^2 - XX - YYYY) - M^2, T = 16 YYYY,
+//   U = (M + E)^2 - M^2 - E^2 - T, X3 = 4 (x E^2 - 4 YY U), Y3 = 8 y (U (T - U) - E E^2), Z3 = 2E.
+// 7S + two two-product reductions + 1M, where the fast ladders' first two steps (|u| starts with the
+// bits 11: a doubling from Z = 1, then a mixed addition) took 3S + 2M + a multiply-plus-square and
+// 3S + 6M + a two-product reduction. Only the endomorphism tests use it (points ON the curve, where
+// any formula for 3P gives the same point); the reference-algorithm ladder keeps ark's operations.
+// In: x any ladder value (the second G1 ladder's base Q1.X is lazy), y limbs < 2^30. Out: X3 limbs
+// < 2^30, Y3 and Z3 normalized. Bounds: tests/field_bounds_model.py jac_tpl_affine_fp.
+KZG_DEV void jac_tpl_affine(jac<fp>& p) {
+  fp x, xx, yy, yyyy, m, mm, s, e, ee, t, u, n, w;
+  fp_norm(x, p.x);                              // x                      N
+  fp_sqr(xx, x);                                // XX                     N
+  fp_sqr(yy, p.y);                              // YY                     N
+  fp_sqr(yyyy, yy);                             // YYYY                   N
+  fp_mul3_nr(m, xx);
+  fp_norm(m, m);                                // M = 3 XX               N
+  fp_sqr(mm, m);                                // MM                     N
+  fp_add_nr(s, x, yy);
+  fp_sqr(s, s);                                 // S1 = (x + YY)^2        N
+  fp_subk_nr<BlsFp::KB_8_28>(s, s, xx);
+  fp_subk_nr<BlsFp::KB_8_28>(s, s, yyyy);
+  fp_norm(w, s);                                // w = S1 - XX - YYYY = 2 x YY   N
+  fp_shl_nr<1>(s, w);
+  fp_mul3_nr(s, s);                             // 6w
+  fp_subk_nr<BlsFp::KB_8_28>(s, s, mm);
+  fp_norm(e, s);                                // E = 6w - MM            N
+  fp_sqr(ee, e);                                // EE                     N
+  fp_shl_nr<3>(t, yyyy);
+  fp_norm(t, t);
+  fp_shl_nr<1>(t, t);                           // T = 16 YYYY           < 2^29
+  fp_add_nr(s, m, e);
+  fp_sqr(s, s);                                 // S2 = (M + E)^2         N
+  fp_subk_nr<BlsFp::KB_8_28>(s, s, mm);
+  fp_subk_nr<BlsFp::KB_16_28>(s, s, ee);
+  fp_subk_nr<BlsFp::KB_32_29>(s, s, t);
+  fp_norm(u, s);                                // U = S2 - MM - EE - T   N
+  fp_negk_nr<BlsFp::KB_128_28>(n, u);           // -U                    < 2^29
+  fp_shl_nr<2>(w, yy);                          // 4 YY                  < 2^30
+  fp_mul_sum2(s, x, ee, w, n);                  // x EE - 4 YY U          N
+  fp_shl_nr<2>(p.x, s);                         // X3                    < 2^30
+  fp_subk_nr<BlsFp::KB_128_28>(w, t, u);        // T - U                 < 2^30
+  fp_negk_nr<BlsFp::KB_16_28>(n, ee);           // -EE                   < 2^29
+  fp_mul_sum2(s, u, w, e, n);                   // U (T - U) - E EE       N
+  fp_mul(s, p.y, s);
+  fp_shl_nr<3>(s, s);
+  fp_norm(p.y, s);                              // Y3 = 8 y (...)         N
+  fp_shl_nr<1>(s, e);
+  fp_norm(p.z, s);                              // Z3 = 2E                N
 }
 
 // ---------------------------------------------------------------- Fp2, carry-free (G2 ladders)
@@ -256,18 +302,22 @@ KZG_DEV void jac_madd(jac<F>& p, Load&& load) {
 }
 
 // [|u|] B for the affine finite base B delivered by load(x, y): 63 doublings, 5 mixed additions.
-// G1: the first doubling starts from Z = 1 (jac_dbl's z_one: no Z multiply). G2 keeps the multiply:
-// 2Y may reach 2.02 p, past what the mixed addition's borrowed constants dominate.
+// G1: |u| starts with the bits 11, so the first doubling and mixed addition are one tripling from
+// the affine base (jac_tpl_affine); then 61 doublings, 4 mixed additions.
 template <typename F, typename Load>
 KZG_DEV void mul_abs_u_affine(jac<F>& acc, Load&& load) {
+  static_assert(((BLS_ABS_U >> (BLS_ABS_U_BITS - 2)) & 3) == 3, "|u| starts with the bits 11");
   load(acc.x, acc.y);
-  f_one(acc.z);
+  int top = BLS_ABS_U_BITS - 2;
+  if constexpr (__is_same(F, fp)) {
+    jac_tpl_affine(acc);  // [3] B
+    top = BLS_ABS_U_BITS - 3;
+  } else {
+    f_one(acc.z);
+  }
 #pragma unroll 1
-  for (int b = BLS_ABS_U_BITS - 2; b >= 0; b--) {
-    if constexpr (__is_same(F, fp))
-      jac_dbl(acc, b == BLS_ABS_U_BITS - 2);
-    else
-      jac_dbl(acc);
+  for (int b = top; b >= 0; b--) {
+    jac_dbl(acc);
     if ((BLS_ABS_U >> b) & 1) jac_madd(acc, load);
   }
 }

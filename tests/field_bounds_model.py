@@ -343,6 +343,33 @@ def jac_dbl_fp(X, Y, Z):
     return x3, y3, z3
 
 
+def jac_tpl_affine_fp(x, y):
+    """jac_tpl_affine(jac<fp>&) — 3P from the affine base (x, y): tpl-2007-bl with Z1 = 1 (Z3 = 2E),
+    7S + 2 two-product reductions + 1M, the lazy forms of curve.hpp."""
+    x = norm(x, "x")  # the second G1 ladder's base Q1.X is a lazy ladder value
+    xx = sqr(x, "XX")
+    yy = sqr(y, "YY")
+    yyyy = sqr(yy, "YYYY")
+    m = norm(mul3(xx), "M")
+    mm = sqr(m, "MM")
+    s1 = sqr(add_nr(x, yy), "S1")
+    w = norm(subk(subk(s1, xx, "KB_8_28", "S1-XX"), yyyy, "KB_8_28", "S1-XX-YYYY"), "2 x YY")
+    e = norm(subk(mul3(shl(w, 1)), mm, "KB_8_28", "6w-MM"), "E")
+    ee = sqr(e, "EE")
+    t = shl(norm(shl(yyyy, 3), "8 YYYY"), 1)  # T = 16 YYYY   < 2^29
+    s2 = sqr(add_nr(m, e), "S2")
+    u = subk(subk(subk(s2, mm, "KB_8_28", "S2-MM"), ee, "KB_16_28", "-EE"), t, "KB_32_29", "-T")
+    u = norm(u, "U")
+    nu = subk(normalized(0), u, "KB_128_28", "-U")
+    x3 = shl(mul_sum2(x, ee, shl(yy, 2), nu, "x EE - 4 YY U"), 2)
+    tu = subk(t, u, "KB_128_28", "T-U")
+    nee = subk(normalized(0), ee, "KB_16_28", "-EE")
+    inner = mul_sum2(u, tu, e, nee, "U (T - U) - E EE")
+    y3 = norm(shl(mul(y, inner, "y inner"), 3), "Y3")
+    z3 = norm(shl(e, 1), "Z3=2E")
+    return x3, y3, z3
+
+
 def jac_dbl(F, X, Y, Z):
     return jac_dbl_fp2_lz(X, Y, Z) if F.two else jac_dbl_fp(X, Y, Z)
 
@@ -416,21 +443,21 @@ def ladder_invariant(F, base_x, base_y, rounds=12):
     """A bound set S for the ladder accumulator (X, Y, Z) that contains the starting point and is
     CLOSED under one ladder step (dbl, then optionally madd(base)) — hence bounds every state
     reached by mul_abs_u_affine / in_subgroup_ref for any input. Found by joined iteration, then
-    inflated and verified closed. For G1 the set also contains mul_abs_u_affine's first step, whose
-    doubling starts from Z = 1 and sets Z3 = norm(2Y) without a multiply (jac_dbl z_one)."""
+    inflated and verified closed. For G1 the set also contains the fast ladder's first step, the
+    tripling of the affine base (jac_tpl_affine: |u| starts with bits 11)."""
     X, Y, Z = base_x, base_y, F.one()
 
-    def step(X, Y, Z, z_one=False):
+    def step(X, Y, Z):
         x1, y1, z1 = jac_dbl(F, X, Y, Z)
-        if z_one and not F.two:
-            z1 = norm(shl(Y, 1), "Z3=2Y")
         outs = [(x1, y1, z1), jac_madd(F, x1, y1, z1, base_x, base_y)]
         nx, ny, nz = X, Y, Z
         for ox, oy, oz in outs:
             nx, ny, nz = join(F, nx, ox), join(F, ny, oy), join(F, nz, oz)
         return nx, ny, nz
 
-    X, Y, Z = step(X, Y, Z, z_one=not F.two)
+    if not F.two:
+        tx, ty, tz = jac_tpl_affine_fp(base_x, base_y)
+        X, Y, Z = join(F, X, tx), join(F, Y, ty), join(F, Z, tz)
 
     for _ in range(rounds):
         X, Y, Z = step(X, Y, Z)

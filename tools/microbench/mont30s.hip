@@ -86,6 +86,72 @@ __device__ __forceinline__ void sqr30(int32_t (&r)[N30], const int32_t (&a)[N30]
   r[N - 1] = (int32_t)acc;
 }
 
+// a b + c as an opaque v_mad_i64_i32 (carry-out to a scratch SGPR pair): a chain of these is not
+// re-associated, so each upper column merges its a*b products onto the carry with one add fewer
+__device__ __forceinline__ int64_t mad_v(int32_t a, int32_t b, int64_t c) {
+  int64_t r;
+  uint64_t dummy;
+  asm("v_mad_i64_i32 %0, %1, %2, %3, %4" : "=v"(r), "=s"(dummy) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+// variants with the upper columns chained on the carry (V = 4: mul30c, 5: sqr30c)
+__device__ __forceinline__ void mul30c(int32_t (&r)[N30], const int32_t (&a)[N30], const int32_t (&b)[N30]) {
+  constexpr int N = N30;
+  int32_t m[N];
+  int64_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < 2 * N - 1; i++) {
+    const int j0 = i < N ? 0 : i - (N - 1);
+    const int j1 = i < N ? i - 1 : N - 1;
+    int64_t accp = 0;
+    if (i >= N) acc += (int64_t)1 << 29;
+#pragma unroll
+    for (int j = j0; j <= j1; j++) {
+      acc = i >= N ? mad_v(a[j], b[i - j], acc) : acc + (int64_t)a[j] * b[i - j];
+      accp += (int64_t)m[j] * P30[i - j];
+    }
+    if (i < N) {
+      acc += (int64_t)a[i] * b[0];
+      acc += accp;
+      m[i] = sext30((uint32_t)acc * PINV30);
+      acc += (int64_t)m[i] * P30[0];
+    } else {
+      acc += accp;
+      r[i - N] = (int32_t)((uint32_t)acc & M30) - (1 << 29);
+    }
+    acc >>= 30;
+  }
+  r[N - 1] = (int32_t)acc;
+}
+__device__ __forceinline__ void sqr30c(int32_t (&r)[N30], const int32_t (&a)[N30]) {
+  constexpr int N = N30;
+  int32_t d[N], m[N];
+#pragma unroll
+  for (int j = 0; j < N; j++) d[j] = a[j] + a[j];
+  int64_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < 2 * N - 1; i++) {
+    const int j0 = i < N ? 0 : i - (N - 1);
+    const int k1 = i < N ? i - 1 : N - 1;
+    int64_t accp = 0;
+    if (i >= N) acc += (int64_t)1 << 29;
+#pragma unroll
+    for (int j = j0; 2 * j < i; j++) acc = i >= N ? mad_v(a[j], d[i - j], acc) : acc + (int64_t)a[j] * d[i - j];
+    if ((i & 1) == 0) acc = i >= N ? mad_v(a[i / 2], a[i / 2], acc) : acc + (int64_t)a[i / 2] * a[i / 2];
+#pragma unroll
+    for (int k = j0; k <= k1; k++) accp += (int64_t)m[k] * P30[i - k];
+    acc += accp;
+    if (i < N) {
+      m[i] = sext30((uint32_t)acc * PINV30);
+      acc += (int64_t)m[i] * P30[0];
+    } else {
+      r[i - N] = (int32_t)((uint32_t)acc & M30) - (1 << 29);
+    }
+    acc >>= 30;
+  }
+  r[N - 1] = (int32_t)acc;
+}
+
 using kzgpot::fp;
 constexpr int N28 = kzgpot::NL;
 
@@ -130,6 +196,8 @@ __global__ void __launch_bounds__(256) kbench(uint32_t* out, const uint32_t* in,
 #pragma unroll
       for (int c = 0; c < CH; c++) {
         if (V == 3) sqr30(x[c], x[c]);
+        else if (V == 5) sqr30c(x[c], x[c]);
+        else if (V == 4) mul30c(x[c], x[c], y);
         else mul30(x[c], x[c], y);
       }
     }
@@ -151,6 +219,10 @@ __global__ void kcheck30(int32_t* out, const int32_t* in) {
   for (int j = 0; j < N30; j++) out[t * 52 + j] = a[j], out[t * 52 + 13 + j] = b[j], out[t * 52 + 26 + j] = r[j];
   sqr30(r, a);
   for (int j = 0; j < N30; j++) out[t * 52 + 39 + j] = r[j];
+  int32_t r2[N30];
+  mul30c(r2, a, b);
+  sqr30c(r, a);
+  for (int j = 0; j < N30; j++) out[256 * 52 + t * 26 + j] = r2[j], out[256 * 52 + t * 26 + 13 + j] = r[j];
 }
 
 int main(int argc, char** argv) {
@@ -162,7 +234,7 @@ int main(int argc, char** argv) {
   uint64_t s = 0x9e3779b97f4a7c15ULL;
   for (int i = 0; i < 4096; i++) { s = s * 6364136223846793005ULL + 1; hin[i] = (uint32_t)(s >> 32); }
   {  // check inputs: random balanced limbs, plus extreme lanes (every limb at -2^29 or 2^29 - 1)
-    static int32_t cin[256 * 26], cout[256 * 52];
+    static int32_t cin[256 * 26], cout[256 * 52 + 256 * 26];
     for (int t = 0; t < 256; t++)
       for (int j = 0; j < 26; j++) {
         const int k = j % 13;
@@ -188,9 +260,9 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
-  const char* nm[4] = {"fp_mul 14x28", "fp_sqr 14x28", "mul30 13x30s", "sqr30 13x30s"};
+  const char* nm[6] = {"fp_mul 14x28", "fp_sqr 14x28", "mul30 13x30s", "sqr30 13x30s", "mul30 chained", "sqr30 chained"};
   for (int pass = 0; pass < 2; pass++)
-    for (int v = 0; v < 4; v++)
+    for (int v = 0; v < 6; v++)
       for (int ch = 1; ch <= 2; ch++)
         for (int occ = 2; occ <= 4; occ += 2) {
           const size_t lds = (160 * 1024) / occ - 1024;
@@ -203,11 +275,15 @@ int main(int argc, char** argv) {
             if (v == 1) L(1, 1);
             if (v == 2) L(2, 1);
             if (v == 3) L(3, 1);
+            if (v == 4) L(4, 1);
+            if (v == 5) L(5, 1);
           } else {
             if (v == 0) L(0, 2);
             if (v == 1) L(1, 2);
             if (v == 2) L(2, 2);
             if (v == 3) L(3, 2);
+            if (v == 4) L(4, 2);
+            if (v == 5) L(5, 2);
           }
 #undef L
           CHECK(hipEventRecord(e1));

@@ -15,7 +15,7 @@ def main(path):
     data = open(path, "rb").read()
     words = struct.unpack("<%di" % (len(data) // 4), data)
     bad = 0
-    lanes = len(words) // 52
+    lanes = 256
     for t in range(lanes):
         w = words[t * 52:(t + 1) * 52]
         a, b, rm, rs = w[0:13], w[13:26], w[26:39], w[39:52]
@@ -24,7 +24,11 @@ def main(path):
             ok = ok and all(-(1 << 29) <= x < (1 << 29) for x in r[:12])
             if not ok:
                 bad += 1
-    print(f"mont30s check: {bad} mismatches over {2 * lanes} products")
+        ext = words[256 * 52 + t * 26:256 * 52 + t * 26 + 26]
+        for r, want in ((ext[0:13], val(a) * val(b)), (ext[13:26], val(a) * val(a))):
+            if (val(r) * R - want) % P != 0 or not all(-(1 << 29) <= x < (1 << 29) for x in r[:12]):
+                bad += 1
+    print(f"mont30s check: {bad} mismatches over {4 * lanes} products")
     return 1 if bad else 0
 
 
