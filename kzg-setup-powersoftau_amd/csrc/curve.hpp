@@ -152,6 +152,10 @@ KZG_DEV void f2_shl(fp2& r, const fp2& a) {
   fp_shl_nr<S>(r.c0, a.c0);
   fp_shl_nr<S>(r.c1, a.c1);
 }
+KZG_DEV void f2_add_nr(fp2& r, const fp2& a, const fp2& b) {
+  fp_add_nr(r.c0, a.c0, b.c0);
+  fp_add_nr(r.c1, a.c1, b.c1);
+}
 KZG_DEV void f2_norm(fp2& r, const fp2& a) {
   fp_norm(r.c0, a.c0);
   fp_norm(r.c1, a.c1);
@@ -196,6 +200,57 @@ KZG_DEV void jac_dbl(jac<fp2>& p) {
   p.y.c0 = c0;                               // Y3 = E (D - X3) - 8 B^2
 }
 
+// G2 tripling from the affine base, as the G1 one (EFD tpl-2007-bl with Z1 = 1) but returned as
+// the equivalent triple (X3/4, Y3/8, Z3/2) = (x EE - 4 YY U, y (U (T - U) - E EE), E), which drops
+// the final x4 / x8 / x2 and their normalizations, and with E = 12 x YY - MM from a product
+// instead of (x + YY)^2 - XX - YYYY: a multiply for a squaring, but E's value stays ~14 p, small
+// enough to serve as Z (the doubling's and the mixed addition's borrowed constants for Z are
+// KB_16_28). The base is fetched twice (load), so that x and y are not held across the formula:
+// at most five Fp2 values live. Out: normalized. Bounds: tests/field_bounds_model.py
+// jac_tpl_affine_fp2_lz (joined into ladder_invariant_fp2_lz).
+template <typename Load>
+KZG_DEV void jac_tpl_affine(jac<fp2>& p, Load&& load) {
+  fp2 yy, m, s, ee, t;
+  load(p.x, p.y);
+  f2_sqr_lz<BlsFp::KB_2_28>(m, p.x);         // XX
+  f2_sqr_lz<BlsFp::KB_2_28>(yy, p.y);        // YY
+  f2_mul_lz<BlsFp::KB_2_28>(p.z, p.x, yy);   // x YY                (x, y dead)
+  fp_mul3_nr(m.c0, m.c0);
+  fp_mul3_nr(m.c1, m.c1);
+  f2_norm(m, m);                             // M = 3 XX
+  f2_sqr_lz<BlsFp::KB_4_28>(t, m);           // MM
+  fp_mul3_nr(p.z.c0, p.z.c0);
+  fp_mul3_nr(p.z.c1, p.z.c1);
+  f2_shl<2>(p.z, p.z);
+  f2_subk<BlsFp::KB_2_28>(p.z, p.z, t);
+  f2_norm(p.z, p.z);                         // E = 12 x YY - MM = Z3
+  f2_add_nr(s, m, p.z);
+  f2_norm(s, s);
+  f2_sqr_lz<BlsFp::KB_32_28>(s, s);          // S2 = (M + E)^2
+  f2_subk<BlsFp::KB_2_28>(s, s, t);          // - MM
+  f2_sqr_lz<BlsFp::KB_16_28>(ee, p.z);       // EE
+  f2_subk<BlsFp::KB_4_28>(s, s, ee);         // - EE
+  f2_sqr_lz<BlsFp::KB_2_28>(t, yy);          // YYYY
+  f2_shl<3>(t, t);
+  f2_norm(t, t);
+  f2_shl<1>(t, t);                           // T = 16 YYYY
+  f2_subk<BlsFp::KB_32_29>(s, s, t);
+  f2_norm(s, s);                             // U = S2 - MM - EE - T
+  f2_subk<BlsFp::KB_64_28>(t, t, s);
+  f2_norm(t, t);                             // T - U
+  f2_mul_lz<BlsFp::KB_128_28>(t, s, t);      // U (T - U)
+  f2_shl<2>(yy, yy);
+  f2_mul_lz<BlsFp::KB_64_28>(yy, yy, s);     // 4 YY U
+  f2_mul_lz<BlsFp::KB_2_28>(m, p.z, ee);     // E EE
+  f2_subk<BlsFp::KB_2_28>(t, t, m);
+  f2_norm(t, t);                             // U (T - U) - E EE
+  load(p.x, p.y);
+  f2_mul_lz<BlsFp::KB_2_28>(p.x, p.x, ee);   // x EE
+  f2_subk<BlsFp::KB_2_28>(p.x, p.x, yy);
+  f2_norm(p.x, p.x);                         // X3 / 4 = x EE - 4 YY U
+  f2_mul_lz<BlsFp::KB_8_28>(p.y, p.y, t);    // Y3 / 8 = y (U (T - U) - E EE)
+}
+
 // G2 mixed addition (ark add_assign_mixed incl. its zero / equal-point branches, as jac_madd):
 // X, Y, Z normalized in and out; the base point (x2, y2) normalized, values < 1.01 p.
 template <typename Load>
@@ -204,11 +259,11 @@ KZG_DEV void jac_madd(jac<fp2>& p, Load&& load) {
   {
     fp2 x2, y2;
     load(x2, y2);
-    f2_sqr_lz<BlsFp::KB_2_28>(z1z1, p.z);
+    f2_sqr_lz<BlsFp::KB_16_28>(z1z1, p.z);   // (Z values reach ~14 p: the tripling's Z3 = E)
     f2_mul_lz<BlsFp::KB_2_28>(h, x2, z1z1);  // U2
     f2_subk<BlsFp::KB_32_28>(h, h, p.x);
     f2_norm(h, h);                           // H = U2 - X1
-    f2_mul_lz<BlsFp::KB_2_28>(t, y2, p.z);
+    f2_mul_lz<BlsFp::KB_16_28>(t, y2, p.z);
     f2_mul_lz<BlsFp::KB_2_28>(t, t, z1z1);   // S2
     f2_subk<BlsFp::KB_32_28>(r, t, p.y);
     f2_norm(r, r);                           // r' = S2 - Y1   (ark's r = 2 r')
@@ -301,22 +356,20 @@ KZG_DEV void jac_madd(jac<F>& p, Load&& load) {
   p.x = t;
 }
 
-// [|u|] B for the affine finite base B delivered by load(x, y): 63 doublings, 5 mixed additions.
-// G1: |u| starts with the bits 11, so the first doubling and mixed addition are one tripling from
-// the affine base (jac_tpl_affine); then 61 doublings, 4 mixed additions.
+// [|u|] B for the affine finite base B delivered by load(x, y): |u| starts with the bits 11, so
+// the first doubling and mixed addition are one tripling from the affine base (jac_tpl_affine);
+// then 61 doublings, 4 mixed additions.
 template <typename F, typename Load>
 KZG_DEV void mul_abs_u_affine(jac<F>& acc, Load&& load) {
   static_assert(((BLS_ABS_U >> (BLS_ABS_U_BITS - 2)) & 3) == 3, "|u| starts with the bits 11");
-  load(acc.x, acc.y);
-  int top = BLS_ABS_U_BITS - 2;
   if constexpr (__is_same(F, fp)) {
+    load(acc.x, acc.y);
     jac_tpl_affine(acc);  // [3] B
-    top = BLS_ABS_U_BITS - 3;
   } else {
-    f_one(acc.z);
+    jac_tpl_affine(acc, load);
   }
 #pragma unroll 1
-  for (int b = top; b >= 0; b--) {
+  for (int b = BLS_ABS_U_BITS - 3; b >= 0; b--) {
     jac_dbl(acc);
     if ((BLS_ABS_U >> b) & 1) jac_madd(acc, load);
   }
@@ -339,11 +392,11 @@ KZG_DEV bool jac_eq_affine(const jac<F>& p, const F& x, const F& y) {
 // The same test on a carry-free G2 ladder state; x, y reduced or normalized with value < 1.01 p.
 KZG_DEV bool jac_eq_affine(const jac<fp2>& p, const fp2& x, const fp2& y) {
   fp2 z2, t;
-  f2_sqr_lz<BlsFp::KB_2_28>(z2, p.z);
+  f2_sqr_lz<BlsFp::KB_16_28>(z2, p.z);
   f2_mul_lz<BlsFp::KB_2_28>(t, x, z2);
   f2_subk<BlsFp::KB_32_28>(t, t, p.x);
   bool ok = f_is_zero(t);
-  f2_mul_lz<BlsFp::KB_2_28>(z2, z2, p.z);
+  f2_mul_lz<BlsFp::KB_16_28>(z2, z2, p.z);
   f2_mul_lz<BlsFp::KB_2_28>(t, y, z2);
   f2_subk<BlsFp::KB_32_28>(t, t, p.y);
   ok = ok && f_is_zero(t);

@@ -529,12 +529,43 @@ def jac_dbl_fp2_lz(X, Y, Z):
     return x3, V2(y0, y1), z3
 
 
+def add2(a, b, name="add2"):
+    return V2(add_nr(a.c0, b.c0, name), add_nr(a.c1, b.c1, name))
+
+
+def jac_tpl_affine_fp2_lz(x, y):
+    """curve.hpp jac_tpl_affine(jac<fp2>&): 3P from the normalized affine base (x, y), returned as
+    the equivalent Jacobian triple (X3/4, Y3/8, Z3/2) = (x EE - 4 YY U, y (U (T - U) - E EE), E),
+    with E = 12 x YY - MM from a product (value ~14 p: Z must stay below 16 p for the doubling's
+    borrowed constant); outputs normalized (the G2 ladder discipline)."""
+    xx = sqr2(x, "KB_2_28", "XX")
+    yy = sqr2(y, "KB_2_28", "YY")
+    yyyy = sqr2(yy, "KB_2_28", "YYYY")
+    m = norm2(mul3_2(xx), "M")
+    mm = sqr2(m, "KB_4_28", "MM")
+    w = mul2(x, yy, "KB_2_28", "x YY")
+    e = norm2(subk2(shl2(mul3_2(w), 2), mm, "KB_2_28", "12 x YY - MM"), "E")
+    ee = sqr2(e, "KB_16_28", "EE")
+    t = shl2(norm2(shl2(yyyy, 3), "8YYYY"), 1)
+    s2 = sqr2(norm2(add2(m, e), "M+E"), "KB_32_28", "S2")
+    u = subk2(subk2(subk2(s2, mm, "KB_2_28", "S2-MM"), ee, "KB_4_28", "-EE"), t, "KB_32_29", "-T")
+    u = norm2(u, "U")
+    a = mul2(x, ee, "KB_2_28", "xEE")
+    b = mul2(shl2(yy, 2), u, "KB_64_28", "4YYU")
+    x3 = norm2(subk2(a, b, "KB_2_28", "xEE-4YYU"), "X3/4")
+    c = mul2(u, norm2(subk2(t, u, "KB_64_28", "T-U"), "T-U"), "KB_128_28", "U(T-U)")
+    d = mul2(e, ee, "KB_2_28", "E EE")
+    inner = norm2(subk2(c, d, "KB_2_28", "inner"), "inner")
+    y3 = mul2(y, inner, "KB_8_28", "Y3/8")
+    return x3, y3, e
+
+
 def jac_madd_fp2_lz(X, Y, Z, x2, y2):
     """curve.hpp jac_madd(jac<fp2>&, load): normalized in / out; base (x2, y2) normalized."""
-    z1z1 = sqr2(Z, "KB_2_28", "Z1Z1")
+    z1z1 = sqr2(Z, "KB_16_28", "Z1Z1")
     u2 = mul2(x2, z1z1, "KB_2_28", "U2")
     h = norm2(subk2(u2, X, "KB_32_28", "H"), "H")
-    t = mul2(y2, Z, "KB_2_28", "y2Z")
+    t = mul2(y2, Z, "KB_16_28", "y2Z")
     s2 = mul2(t, z1z1, "KB_2_28", "S2")
     r = norm2(subk2(s2, Y, "KB_32_28", "r'"), "r'")
     zero_ok2(Z, "Z"), zero_ok2(h, "H"), zero_ok2(r, "r'")
@@ -558,10 +589,10 @@ def jac_madd_fp2_lz(X, Y, Z, x2, y2):
 
 def jac_eq_affine_fp2_lz(X, Y, Z, x, y):
     """curve.hpp jac_eq_affine(const jac<fp2>&, ..): x Z^2 == X, y Z^3 == Y, Z != 0."""
-    z2 = sqr2(Z, "KB_2_28", "z2")
+    z2 = sqr2(Z, "KB_16_28", "z2")
     t = subk2(mul2(x, z2, "KB_2_28", "xZ2"), X, "KB_32_28", "eqx")
     zero_ok2(t, "eqx")
-    z3 = mul2(z2, Z, "KB_2_28", "z3")
+    z3 = mul2(z2, Z, "KB_16_28", "z3")
     t = subk2(mul2(y, z3, "KB_2_28", "yZ3"), Y, "KB_32_28", "eqy")
     zero_ok2(t, "eqy")
     zero_ok2(Z, "Z")
@@ -588,6 +619,8 @@ def ladder_invariant_fp2_lz(base_x, base_y, rounds=12):
         return nx, ny, nz
 
     X, Y, Z = base_x, base_y, V2(normalized(1), normalized(0))
+    tx, ty, tz = jac_tpl_affine_fp2_lz(base_x, base_y)  # the fast ladder's first step: 3 B
+    X, Y, Z = join2(X, tx), join2(Y, ty), join2(Z, tz)
     for _ in range(rounds):
         X, Y, Z = step(X, Y, Z)
     S = (infl(X), infl(Y), infl(Z))
