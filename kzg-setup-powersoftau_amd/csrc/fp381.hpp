@@ -259,9 +259,19 @@ KZG_DEV uint32_t lit_sub(uint32_t b) {
   asm("v_sub_u32_e32 %0, %1, %2" : "=v"(r) : "n"(C), "v"(b));
   return r;
 }
+// a + C, the same way. a + K - b is formed as (a + K) - b rather than a + (K - b): K - b would
+// depend on b alone, and the scheduler then hoists it (for the G2 mixed addition's H = U2 - X1 and
+// r' = S2 - Y1: to the end of the preceding doubling), where the 2 x 14 results occupied VGPRs
+// across the whole multiply chain and were spilled to scratch at every ladder step.
+template <uint32_t C>
+KZG_DEV uint32_t lit_add(uint32_t a) {
+  uint32_t r;
+  asm("v_add_u32_e32 %0, %1, %2" : "=v"(r) : "n"(C), "v"(a));
+  return r;
+}
 template <const auto& K, class Tr, size_t... I>
 KZG_DEV void subk_lit(Fe<Tr>& r, const Fe<Tr>& a, const Fe<Tr>& b, std::index_sequence<I...>) {
-  ((r.v[I] = a.v[I] + lit_sub<K[I]>(b.v[I])), ...);
+  ((r.v[I] = lit_add<K[I]>(a.v[I]) - b.v[I]), ...);
 }
 template <const auto& K, class Tr, size_t... I>
 KZG_DEV void negk_lit(Fe<Tr>& r, const Fe<Tr>& b, std::index_sequence<I...>) {
@@ -744,9 +754,8 @@ KZG_DEV void f_norm(fp& r, const fp& a) { fp_norm(r, a); }
 // 3 full multiplies, but none of Karatsuba's serial borrow / carry / conditional-2p chains
 // (two fp_sub_red, one fp_add_red). Reduced in, reduced out (value < 1.01 p).
 KZG_DEV void f_mul(fp2& r, const fp2& a, const fp2& b) {
-  fp nb1, zero, c0;
-  fp_zero(zero);
-  fp_subk_nr<BlsFp::KB_4_28>(nb1, zero, b.c1);  // 4p - b1, limbs < 2^29
+  fp nb1, c0;
+  fp_negk_nr<BlsFp::KB_4_28>(nb1, b.c1);  // 4p - b1, limbs < 2^29
   fp_mul_sum2(c0, a.c0, b.c0, a.c1, nb1);
   fp_mul_sum2(r.c1, a.c0, b.c1, a.c1, b.c0);
   r.c0 = c0;
