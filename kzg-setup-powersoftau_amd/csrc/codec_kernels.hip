@@ -219,8 +219,9 @@ __global__ void __launch_bounds__(kBlock) k_g1_codec(const uint4* __restrict__ i
 // rule normalises it). With N = a0^2 + a1^2 (a is a square in Fp2 iff N is one in Fp):
 //   gam = sqrt(N); d = (a0 + gam)/2 (d = a0 if that is 0); t = d^((p-3)/4); s = t d
 //   s^2 == d  ->  y = (s, a1 t / 2)      else (s^2 = -d, t s = -1)  ->  y = (-a1 t / 2, s)
-// and y is accepted iff gam^2 == N and y^2 == a. Two Fp exponentiations (~920 Fp multiplies)
-// where Algorithm 9 needs two Fp2 ones (~2,700). In: a reduced; out: y reduced.
+// and y is accepted iff y^2 == a (no separate gam^2 == N test: a non-square a has no y with
+// y^2 = a, and a square a has a square norm). Two Fp exponentiations (~920 Fp multiplies) where
+// Algorithm 9 needs two Fp2 ones (~2,700). In: a reduced; out: y reduced.
 KZG_DEV bool fp2_sqrt(fp2& y, const fp2& a) {
   fp nrm, t0, gam, d, s, h, inv2;
   fp_sqr(nrm, a.c0);
@@ -228,8 +229,6 @@ KZG_DEV bool fp2_sqrt(fp2& y, const fp2& a) {
   fp_add_nr(nrm, nrm, t0);
   fp_pow_pm3d4(t0, nrm);
   fp_mul(gam, t0, nrm);
-  fp_sqr(t0, gam);
-  const bool ok1 = fp_eq(t0, nrm);
   fp_set(inv2, FP_INV2);
   fp_add_nr(d, a.c0, gam);
   fp_mul(d, d, inv2);
@@ -249,7 +248,7 @@ KZG_DEV bool fp2_sqrt(fp2& y, const fp2& a) {
   f_sqr(y2, y);
   fp_sub_red(y2.c0, y2.c0, a.c0);
   fp_sub_red(y2.c1, y2.c1, a.c1);
-  return ok1 && f_is_zero(y2);
+  return f_is_zero(y2);
 }
 
 // x^3 + 4 (1 + u), reduced
