@@ -10,6 +10,8 @@ on subgroup points, on random curve points outside the subgroup and on small-ord
   jac_tpl_affine (G1)     EFD tpl-2007-bl with Z1 = 1: (X3, Y3, 2E)
   jac_tpl_affine (G2)     the equivalent triple (X3 / 4, Y3 / 8, E), E = 12 x YY - MM
   mul_abs_u_affine        [|u|] B: the tripling, then 61 doublings and 4 mixed additions
+  in_subgroup_fast_g1     [u^2] P as [|u|] of Q1 = (X : Y : Z) run on y^2 = x^3 + 4 Z^6 from the
+                          affine (X, Y), mapped back by Z' -> Z' Z; compared with phi(P) = (beta x, -y)
 """
 import random
 
@@ -134,20 +136,24 @@ def tpl_g2(x, y):
     return x3, y3, e
 
 
-def mul_abs_u(F, dbl, tpl, base):
+def mul_abs_u_jac(F, dbl, tpl, base):
     X, Y, Z = tpl(*base)
     for b in range(ABS_U.bit_length() - 3, -1, -1):
         X, Y, Z = dbl(X, Y, Z)
         if (ABS_U >> b) & 1:
             X, Y, Z = madd(F, dbl, X, Y, Z, *base)
-    return affine(F, X, Y, Z)
+    return X, Y, Z
+
+
+def mul_abs_u(F, dbl, tpl, base):
+    return affine(F, *mul_abs_u_jac(F, dbl, tpl, base))
 
 
 def _points(group, rng):
     if group == "g1":
-        gen, mul, rnd, h = O.G1_GEN, O.g1_mul, O.g1_random_on_curve, O.H1
+        gen, mul, rnd = O.G1_GEN, O.g1_mul, O.g1_random_on_curve
     else:
-        gen, mul, rnd, h = O.G2_GEN, O.g2_mul, O.g2_random_on_curve, O.H2
+        gen, mul, rnd = O.G2_GEN, O.g2_mul, O.g2_random_on_curve
     pts = [mul(gen, rng.randrange(1, O.R_ORDER)) for _ in range(4)]
     pts += [rnd(rng) for _ in range(4)]
     # points of the cofactor part: no r component at all
@@ -184,3 +190,18 @@ def test_ladder_abs_u():
     for group, F, dbl, tpl, mul in (("g1", Fp, dbl_g1, tpl_g1, O.g1_mul), ("g2", Fp2, dbl_g2, tpl_g2, O.g2_mul)):
         for pt in _points(group, rng)[:7] + _points(group, rng)[-2:]:
             assert mul_abs_u(F, dbl, tpl, pt) == mul(pt, ABS_U), (group, pt)
+
+
+def test_g1_second_ladder_on_isomorphic_curve():
+    rng = random.Random(4)
+    for pt in _points("g1", rng):
+        X, Y, Z = mul_abs_u_jac(Fp, dbl_g1, tpl_g1, pt)
+        if Z == 0:
+            continue  # Q1 = O: the kernel's second ladder ends in Z' Z = 0 as well
+        X2, Y2, Z2 = mul_abs_u_jac(Fp, dbl_g1, tpl_g1, (X, Y))
+        got = affine(Fp, X2, Y2, Fp.mul(Z2, Z))
+        assert got == O.g1_mul(pt, ABS_U * ABS_U)
+        if O.g1_mul(pt, O.R_ORDER) is None:
+            # on G1, [u^2] P = (beta x, -y) for one of the two primitive cube roots of unity beta
+            b = next(c for c in (pow(g, (P - 1) // 3, P) for g in range(2, 20)) if c != 1)
+            assert got in [((b * pt[0]) % P, (-pt[1]) % P), ((b * b * pt[0]) % P, (-pt[1]) % P)]
