@@ -1,4 +1,5 @@
-// Internal C++ interface between the C ABI (capi.hip) and the kernels (codec_kernels.hip).
+// Internal C++ interface between the C ABI (capi.hip) and the kernels (codec_kernels.hip,
+// g1_kernels.hip).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -45,6 +46,18 @@ constexpr uint64_t out_record(CodecOp op) {
   }
   return 0;
 }
+
+// phase 1 marks a rejected point's record with this value in x's top word (phase 2 then skips it)
+constexpr uint32_t kPoison = 0xffffffffu;
+
+// where phase 2 (k_g1_check / k_g2_check) reads its record (codec_kernels.hip "phase 2")
+enum class Src { ArkInPlace, PairingBE, PairingBEInPlace };
+constexpr bool src_in_place(Src s) { return s != Src::PairingBE; }
+
+// G1 kernels (g1_kernels.hip, its own translation unit: compiled with the iterative ILP scheduler):
+// G1Decompress (fused or split), G1Transcode, and G1Phase1's in-place transcode (in = nullptr)
+hipError_t launch_g1(CodecOp op, const uint4* in, uint4* out, uint64_t n, uint32_t flags,
+                     unsigned long long* d_first_bad, uint8_t* d_status, hipStream_t stream);
 
 // loader kernels (load_kernels.hip)
 hipError_t launch_load(bool g2, const void* d_in, void* d_out, uint64_t n, unsigned long long* d_first_bad,
