@@ -1,5 +1,5 @@
 """Exact interval model of the radix-2^28 field arithmetic in csrc/fp381.hpp and the formulas in
-csrc/curve.hpp / codec_kernels.hip — used by tests/test_field_bounds.py to PROVE (for all inputs)
+csrc/curve.hpp / codec_kernels.hip / g1_kernels.hip — used by tests/test_field_bounds.py to PROVE (for all inputs)
 that no 64-bit column accumulator, 32-bit limb or borrowed-constant subtraction can overflow.
 
 Each value is modelled by per-limb upper bounds (exact ints) and a value upper bound (in units of
