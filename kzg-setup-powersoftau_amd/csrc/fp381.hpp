@@ -364,9 +364,18 @@ KZG_DEV bool fp_is_zero_canon(const Fe<Tr>& c) {
 // (exact to ~1e-14 against a >= 4.6e-8 margin for every k; tests/test_fast_paths_math.py) — so
 // the test is one normalization, NL small MACs and a compare (~130 instructions) instead of the
 // 8-step conditional-subtraction chain (~600).
+// A filter runs first: a = k p forces a = k p (mod 2^LB), and limb 0 of a's normalization is
+// a.v[0] mod 2^LB (no carry comes in), so k can only be (a.v[0] mod 2^LB) p^-1 mod 2^LB — one
+// v_mul_lo. A lane whose candidate is >= 256 holds a nonzero value. A nonzero value passes with
+// probability 2^-20 (BLS) / 2^-21 (BN254), so the wave almost always skips the full test through
+// one wave-uniform branch (the ladders' exceptional-case tests: 24 calls per G1 point).
 template <class Tr>
 KZG_DEV bool fp_is_zero(const Fe<Tr>& a) {
   constexpr int N = Tr::NL;
+  const uint32_t kc = ((a.v[0] & Tr::MASK) * (0u - Tr::PINV)) & Tr::MASK;  // PINV = -p^-1
+  const bool maybe = kc < 256u;
+  if (__builtin_amdgcn_ballot_w64(maybe) == 0) return false;
+  if (!maybe) return false;
   Fe<Tr> n;
   fp_norm(n, a);
   const uint32_t k = (uint32_t)((double)(n.v[N - 1] + 1u) * Tr::INV_RHO);

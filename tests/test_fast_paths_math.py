@@ -110,6 +110,36 @@ def test_fp2_sqrt_equivalence():
 
 
 @pytest.mark.parametrize("hdr,nl,lb", [("bls12_381_consts.hpp", 14, 28), ("bn254_consts.hpp", 9, 29)])
+def test_is_zero_low_limb_filter(hdr, nl, lb):
+    """fp381.hpp fp_is_zero's filter: k_c = (a.v[0] mod 2^lb) (-PINV) mod 2^lb equals k for every
+    a = k p (so no zero is filtered out, whatever the unnormalized limbs above limb 0 hold), and
+    random nonzero values pass it (k_c < 256) about 256 / 2^lb of the time."""
+    import os
+    import random
+    import re
+
+    text = open(os.path.join(os.path.dirname(__file__), "..", "kzg-setup-powersoftau_amd", "csrc", hdr)).read()
+    pinv = int(re.search(r"PINV = (0x[0-9a-f]+)u;", text).group(1), 16)
+    body = re.search(r"uint32_t P\[\d+\] = \{([^}]*)\}", text).group(1)
+    limbs = [int(v.strip().rstrip("u"), 16) for v in body.split(",")]
+    p = sum(v << (lb * i) for i, v in enumerate(limbs))
+    mask = (1 << lb) - 1
+    assert (p * pinv + 1) & mask == 0
+
+    def kc(limb0):
+        return ((limb0 & mask) * ((0 - pinv) & 0xFFFFFFFF) & 0xFFFFFFFF) & mask
+
+    rng = random.Random(9)
+    for k in range(256):
+        a = k * p
+        assert kc(a & mask) == k
+        # the same value with a carry left in limb 0 (limb 0 + 2^lb, limb 1 - 1): limb 0 mod 2^lb is unchanged
+        assert kc((a & mask) + (1 << lb)) == k
+    hits = sum(kc(rng.randrange(1 << 32)) < 256 for _ in range(200000))
+    assert hits < 200000 * 256 / (1 << lb) * 3 + 5
+
+
+@pytest.mark.parametrize("hdr,nl,lb", [("bls12_381_consts.hpp", 14, 28), ("bn254_consts.hpp", 9, 29)])
 def test_is_zero_quotient_estimate(hdr, nl, lb):
     """fp381.hpp fp_is_zero: for every normalized a < min(256 p, R), a == k p with
     k = trunc((top + 1) * INV_RHO) (IEEE double, as on the GPU) iff a == 0 mod p."""
