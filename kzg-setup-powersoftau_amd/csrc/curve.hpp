@@ -116,6 +116,117 @@ KZG_DEV void jac_tpl_affine(jac<fp>& p) {
   fp_norm(p.z, s);                              // Z3 = 2E                N
 }
 
+// ---------------------------------------------------------------- G1 fast ladders, W = 2Y
+// The endomorphism test's ladders (in_subgroup_fast_g1) carry W = 2Y instead of Y: then
+// B' = W^2 = 4B, D = X B' and Z3 = W Z need no 4X / 2Y, and -W3 = 2E (X3 - D) + B'^2 needs no
+// 8 B^2 scaling (fp_mul_addsqr<1>) — per doubling 14 v_lshlrev (4X) and 14 v_lshlrev + 14 adds
+// (8B, 16B) fewer, 14 adds (2 (X3 - D)) more. Every formula is ark's scaled by the exact factor 2
+// on Y, so equal-point and zero tests decide as before; the reference-algorithm ladder
+// (in_subgroup_ref) and the generator keep the Y form. Bounds: tests/field_bounds_model.py
+// jac_dbl_w / jac_madd_w / jac_tpl_affine_w / ladder_invariant_w.
+KZG_DEV void jac_dbl_w(jac<fp>& p) {
+  fp a, b, d, e, t;
+  fp_sqr(a, p.x);              // A = X^2                    N
+  fp_sqr(b, p.y);              // B' = W^2 = 4 Y^2           N
+  fp_mul(d, p.x, b);           // D = X B' = 4 X Y^2         N
+  fp_mul3_nr(e, a);
+  fp_norm(e, e);               // E = 3A                     N
+  fp_mul(p.z, p.y, p.z);       // Z3 = W Z = 2 Y Z           N
+  fp_sqr(a, e);                // F = E^2                    N
+  fp_shl_nr<1>(t, d);          // 2D                        < 2^29
+  fp_subk_nr<BlsFp::KB_8_29>(p.x, a, t);  // X3 = F - 2D           < 2^30 + 2^28
+  fp_mul3_nr(t, d);            // 3D                        < 3 * 2^28
+  fp_subk_nr<BlsFp::KB_8_30>(t, a, t);    // X3 - D = F - 3D       < 2^30 + 2^28
+  fp_shl_nr<1>(t, t);          // 2 (X3 - D)
+  fp_mul_addsqr<1>(d, e, t, b);  // -W3 = E 2 (X3 - D) + B'^2   N
+  fp_negk_nr<BlsFp::KB_2_28>(p.y, d);     // W3                    < 2^29
+}
+
+// 3P from the affine base (x, w = 2y), tpl-2007-bl with Z1 = 1 in W form: YYw = w^2 = 4 YY,
+// T = YYw^2 = 16 YYYY, E = 3 x YYw - MM (= 12 x YY - MM), U = (M + E)^2 - MM - EE - T,
+// X3 = 4 (x EE - YYw U), W3 = 2 Y3 = 8 w (U (T - U) - E EE), Z3 = 2E.
+KZG_DEV void jac_tpl_affine_w(jac<fp>& p) {
+  fp x, xx, yy, m, mm, s, e, ee, t, u, n;
+  fp_norm(x, p.x);                              // x (the second ladder's base Q1.X is lazy)
+  fp_sqr(xx, x);                                // XX                     N
+  fp_sqr(yy, p.y);                              // YYw = w^2              N
+  fp_sqr(t, yy);                                // T = YYw^2 = 16 YYYY    N
+  fp_mul3_nr(m, xx);
+  fp_norm(m, m);                                // M = 3 XX               N
+  fp_sqr(mm, m);                                // MM                     N
+  fp_mul(s, x, yy);                             // x YYw                  N
+  fp_mul3_nr(s, s);
+  fp_subk_nr<BlsFp::KB_8_28>(s, s, mm);
+  fp_norm(e, s);                                // E = 3 x YYw - MM       N
+  fp_sqr(ee, e);                                // EE                     N
+  fp_add_nr(s, m, e);
+  fp_sqr(s, s);                                 // S2 = (M + E)^2         N
+  fp_subk_nr<BlsFp::KB_8_28>(s, s, mm);
+  fp_subk_nr<BlsFp::KB_16_28>(s, s, ee);
+  fp_subk_nr<BlsFp::KB_8_28>(s, s, t);
+  fp_norm(u, s);                                // U = S2 - MM - EE - T   N
+  fp_negk_nr<BlsFp::KB_128_28>(n, u);           // -U                    < 2^29
+  fp_mul_sum2(s, x, ee, yy, n);                 // x EE - YYw U           N
+  fp_shl_nr<2>(p.x, s);                         // X3                    < 2^30
+  fp_subk_nr<BlsFp::KB_128_28>(t, t, u);        // T - U                 < 2^30
+  fp_negk_nr<BlsFp::KB_16_28>(n, ee);           // -EE                   < 2^29
+  fp_mul_sum2(s, u, t, e, n);                   // U (T - U) - E EE       N
+  fp_mul(s, p.y, s);
+  fp_shl_nr<3>(s, s);
+  fp_norm(p.y, s);                              // W3 = 8 w (...)         N
+  fp_shl_nr<1>(s, e);
+  fp_norm(p.z, s);                              // Z3 = 2E                N
+}
+
+// jac_madd in W form: load(x2, w2) delivers the base with w2 = 2 y2. r = 2 S2 - W1 is ark's
+// r = 2 (S2 - Y1), so X3 = r^2 - J - 2V needs no 4 r'^2, and W3 = 2 Y3 = 2r (V - X3) - 2 W1 J.
+template <typename Load>
+KZG_DEV void jac_madd_w(jac<fp>& p, Load&& load) {
+  fp z1z1, h, r, t;
+  {
+    fp x2, w2;
+    load(x2, w2);
+    fp_sqr(z1z1, p.z);
+    fp_mul(h, x2, z1z1);       // U2
+    f_subk<BlsFp::KB_128_31>(h, h, p.x);
+    fp_norm(h, h);             // H = U2 - X1
+    fp_mul(t, w2, p.z);
+    fp_mul(t, t, z1z1);        // 2 S2
+    f_subk<BlsFp::KB_64_31>(r, t, p.y);
+    fp_norm(r, r);             // r = 2 S2 - W1 = 2 (S2 - Y1)
+  }
+  const bool z1zero = fp_is_zero(p.z);
+  const bool same = !z1zero && fp_is_zero(h) && fp_is_zero(r);
+  if (__builtin_expect(z1zero || same, 0)) {
+    if (same) {
+      jac_dbl_w(p);
+    } else {
+      load(p.x, p.y);
+      f_one(p.z);
+    }
+    return;
+  }
+  fp hh, j;
+  fp_sqr(hh, h);               // HH
+  fp_shl_nr<1>(t, p.z);
+  fp_mul(p.z, t, h);           // Z3 = 2 Z1 H
+  fp_shl_nr<2>(hh, hh);
+  fp_norm(hh, hh);             // I = 4 HH
+  fp_mul(j, h, hh);            // J = H I
+  fp_mul(hh, p.x, hh);         // V = X1 I
+  fp_sqr(t, r);                // r^2
+  f_subk<BlsFp::KB_32_28>(t, t, j);
+  fp_shl_nr<1>(h, hh);         // 2V
+  f_subk<BlsFp::KB_64_29>(t, t, h);
+  fp_norm(t, t);               // X3 = r^2 - J - 2V
+  f_subk<BlsFp::KB_128_28>(hh, hh, t);
+  fp_norm(hh, hh);             // V - X3
+  fp_shl_nr<1>(r, r);          // 2r           < 2^29
+  fp_shl_nr<1>(h, p.y);        // 2 W1         < 2^30
+  f_mul_sub(p.y, r, hh, h, j); // W3 = 2r (V - X3) - 2 W1 J
+  p.x = t;
+}
+
 // ---------------------------------------------------------------- Fp2, carry-free (G2 ladders)
 // The G1 discipline on both components: limb-wise adds and borrowed-constant subtractions, an
 // fp_norm only where the next multiply needs normalized limbs — instead of the reduced (< 2p)
@@ -362,16 +473,21 @@ KZG_DEV void jac_madd(jac<F>& p, Load&& load) {
 template <typename F, typename Load>
 KZG_DEV void mul_abs_u_affine(jac<F>& acc, Load&& load) {
   static_assert(((BLS_ABS_U >> (BLS_ABS_U_BITS - 2)) & 3) == 3, "|u| starts with the bits 11");
-  if constexpr (__is_same(F, fp)) {
+  if constexpr (__is_same(F, fp)) {  // W = 2Y form: load delivers (x, 2y)
     load(acc.x, acc.y);
-    jac_tpl_affine(acc);  // [3] B
+    jac_tpl_affine_w(acc);  // [3] B
+#pragma unroll 1
+    for (int b = BLS_ABS_U_BITS - 3; b >= 0; b--) {
+      jac_dbl_w(acc);
+      if ((BLS_ABS_U >> b) & 1) jac_madd_w(acc, load);
+    }
   } else {
     jac_tpl_affine(acc, load);
-  }
 #pragma unroll 1
-  for (int b = BLS_ABS_U_BITS - 3; b >= 0; b--) {
-    jac_dbl(acc);
-    if ((BLS_ABS_U >> b) & 1) jac_madd(acc, load);
+    for (int b = BLS_ABS_U_BITS - 3; b >= 0; b--) {
+      jac_dbl(acc);
+      if ((BLS_ABS_U >> b) & 1) jac_madd(acc, load);
+    }
   }
 }
 // Jacobian (X, Y, Z) == affine (x, y)?  (X == x Z^2, Y == y Z^3, Z != 0). X, Y limbs < 2^30.
@@ -431,7 +547,10 @@ template <typename LoadRow, typename Park, typename LoadQZ>
 KZG_DEV bool in_subgroup_fast_g1(LoadRow&& load_row, Park&& park, LoadQZ&& load_qz) {
   jac<fp> q;
   int src = 0;
-  auto load = [&](fp& bx, fp& by) { load_row(src, bx, by); };
+  auto load = [&](fp& bx, fp& bw) {  // (x, w = 2y): P's row holds y, Q1's row already holds W
+    load_row(src, bx, bw);
+    if (src == 0) fp_shl_nr<1>(bw, bw);
+  };
 #pragma unroll 1
   for (int pass = 0; pass < 2; pass++) {
     src = __builtin_amdgcn_readfirstlane(pass);
@@ -449,6 +568,7 @@ KZG_DEV bool in_subgroup_fast_g1(LoadRow&& load_row, Park&& park, LoadQZ&& load_
   fp_set(beta, FP_BETA);
   fp_mul(x, x, beta);
   fp_neg(y, y);
+  fp_shl_nr<1>(y, y);  // the ladders carry W = 2Y: compare with 2 (-y)
   return jac_eq_affine(q2, x, y);
 }
 

@@ -165,13 +165,16 @@ KZG_DEV void fp_mul_sum3(Fe<Tr>& r, const Fe<Tr>& a, const Fe<Tr>& b, const Fe<T
 // cross products c_j (16 c_k) once, squares c_j (8 c_j) — the G1 doubling's -Y3 = E (X3 - D) + 8 B^2
 // (curve.hpp), 105 instead of 196 mads for the 8 B^2 term. c must be normalized (16 c_k < 2^32);
 // column sums: tests/field_bounds_model.py mul_add8sqr.
-template <class Tr>
-KZG_DEV void fp_mul_add8sqr(Fe<Tr>& r, const Fe<Tr>& a, const Fe<Tr>& b, const Fe<Tr>& c) {
+// fp_mul_addsqr<S>: (a b + S c^2) R^-1 for S = 8 (the Y-form doubling) or S = 1 (the W = 2Y form,
+// whose B'^2 = 16 B^2 needs no scale: curve.hpp jac_dbl_w; bounds field_bounds_model.mul_addsqr).
+template <int S, class Tr>
+KZG_DEV void fp_mul_addsqr(Fe<Tr>& r, const Fe<Tr>& a, const Fe<Tr>& b, const Fe<Tr>& c) {
+  static_assert(S == 1 || S == 8, "scale");
   constexpr int N = Tr::NL;
-  uint32_t c8[N], c16[N], m[N];
+  uint32_t c8[N], c16[N], m[N];  // S c and 2 S c
 #pragma unroll
   for (int j = 0; j < N; j++) {
-    c8[j] = c.v[j] << 3;
+    c8[j] = S == 1 ? c.v[j] : c.v[j] << 3;
     c16[j] = dbl_u32(c8[j]);
   }
   uint64_t acc = 0;
@@ -199,6 +202,10 @@ KZG_DEV void fp_mul_add8sqr(Fe<Tr>& r, const Fe<Tr>& a, const Fe<Tr>& b, const F
     }
     acc >>= Tr::LB;
   }
+}
+template <class Tr>
+KZG_DEV void fp_mul_add8sqr(Fe<Tr>& r, const Fe<Tr>& a, const Fe<Tr>& b, const Fe<Tr>& c) {
+  fp_mul_addsqr<8>(r, a, b, c);
 }
 // r = a^2 R^-1 mod p: each cross product a_j a_k (j < k) once, as a_j (2 a_k), plus the squares —
 // NL(NL+1)/2 instead of NL^2 products for the a*a half (the NL^2 m*p products of the reduction

@@ -160,6 +160,24 @@ def mul_add8sqr(a: V, b: V, c: V, name="mul_add8sqr"):
     return normalized(((a.val * b.val + 8 * c.val * c.val) * P_OVER_R + 1) * UP, name)
 
 
+def mul_addsqr(a: V, b: V, c: V, name="mul_addsqr"):
+    """fp_mul_addsqr<1>: a b + c^2 with one reduction, the c^2 half as a squaring (cross products
+    c_j (2 c_k) once, squares c_j c_j): column sums equal those of a b + c c."""
+    if max(c.limbs) << 1 >= 1 << 32:
+        raise BoundError(f"{name}: 2 c_k must fit 32 bits ({c!r})")
+    carry = 0
+    for i in range(2 * NL):
+        j0 = 0 if i < NL else i - (NL - 1)
+        j1 = i if i < NL else NL - 1
+        s = sum(a.limbs[j] * b.limbs[i - j] + c.limbs[j] * c.limbs[i - j] for j in range(j0, j1 + 1))
+        s += sum(LM * P_L[i - j] for j in range(j0, j1 + 1))
+        s += carry
+        if s >= 1 << 64:
+            raise BoundError(f"{name}: column {i} may reach {s.bit_length()} bits")
+        carry = s >> LB
+    return normalized(((a.val * b.val + c.val * c.val) * P_OVER_R + 1) * UP, name)
+
+
 def sqr(a: V, name="sqr"):
     """fp_sqr: same column sums as mul(a, a); the doubled operand 2 a_k must fit 32 bits."""
     if max(a.limbs) >= 1 << 31:
@@ -368,6 +386,89 @@ def jac_tpl_affine_fp(x, y):
     y3 = norm(shl(mul(y, inner, "y inner"), 3), "Y3")
     z3 = norm(shl(e, 1), "Z3=2E")
     return x3, y3, z3
+
+
+# ---- the G1 fast ladders in W = 2Y coordinates (curve.hpp jac_dbl_w / jac_madd_w / jac_tpl_affine_w)
+def jac_dbl_w(X, W, Z):
+    """jac_dbl_w: A = X^2, B' = W^2, D = X B', E = 3A, Z3 = W Z, X3 = F - 2D,
+    -W3 = E (2 (X3 - D)) + B'^2 (one reduction), W3 = K - that."""
+    a = sqr(X, "A")
+    b = sqr(W, "B'")
+    d = mul(X, b, "D")
+    e = norm(mul3(a), "E")
+    z3 = mul(W, Z, "Z3")
+    f = sqr(e, "F")
+    x3 = subk(f, shl(d, 1), "KB_8_29", "X3")
+    t = shl(subk(f, mul3(d), "KB_8_30", "F-3D"), 1, "2(F-3D)")
+    nw3 = mul_addsqr(e, t, b, "-W3")
+    w3 = subk(normalized(0), nw3, "KB_2_28", "W3")
+    return x3, w3, z3
+
+
+def jac_madd_w(X, W, Z, x2, w2):
+    """jac_madd_w: ark add_assign_mixed with r = 2 S2 - W1 (= ark's r), X3 = r^2 - J - 2V,
+    W3 = 2 r (V - X3) - 2 W1 J; the equal-point branch is jac_dbl_w; base (x2, w2 = 2 y2)."""
+    z1z1 = sqr(Z, "Z1Z1")
+    h = norm(subk(mul(x2, z1z1, "U2"), X, "KB_128_31", "H"), "H")
+    t = mul(mul(w2, Z, "w2Z"), z1z1, "2S2")
+    r = norm(subk(t, W, "KB_64_31", "r"), "r")
+    canon_ok(Z), canon_ok(h), canon_ok(r)
+    xd, wd, zd = jac_dbl_w(X, W, Z)
+    hh = sqr(h, "HH")
+    z3 = mul(shl(Z, 1), h, "Z3")
+    i = norm(shl(hh, 2), "I")
+    j = mul(h, i, "J")
+    v = mul(X, i, "V")
+    t = subk(sqr(r, "r^2"), j, "KB_32_28", "X3a")
+    x3 = norm(subk(t, shl(v, 1), "KB_64_29", "X3"), "X3")
+    vx = norm(subk(v, x3, "KB_128_28", "V-X3"), "V-X3")
+    w3 = mul_sum2(shl(r, 1), vx, shl(W, 1), subk(normalized(0), j, "KB_4_28", "-J"), "W3")
+    return vmax(x3, xd, x2), vmax(w3, wd, w2), vmax(z3, zd, normalized(1))
+
+
+def jac_tpl_affine_w(x, w):
+    """jac_tpl_affine_w: 3P from the affine base (x, w = 2y): YYw = w^2 = 4 YY, T = YYw^2 = 16 YYYY,
+    E = 3 x YYw - MM, X3 = 4 (x EE - YYw U), W3 = 8 w (U (T - U) - E EE), Z3 = 2E."""
+    x = norm(x, "x")
+    xx = sqr(x, "XX")
+    yyw = sqr(w, "YYw")
+    t = sqr(yyw, "T")
+    m = norm(mul3(xx), "M")
+    mm = sqr(m, "MM")
+    e = norm(subk(mul3(mul(x, yyw, "x YYw")), mm, "KB_8_28", "3 x YYw - MM"), "E")
+    ee = sqr(e, "EE")
+    s2 = sqr(add_nr(m, e), "S2")
+    u = subk(subk(subk(s2, mm, "KB_8_28", "S2-MM"), ee, "KB_16_28", "-EE"), t, "KB_8_28", "-T")
+    u = norm(u, "U")
+    nu = subk(normalized(0), u, "KB_128_28", "-U")
+    x3 = shl(mul_sum2(x, ee, yyw, nu, "x EE - YYw U"), 2)
+    tu = subk(t, u, "KB_128_28", "T-U")
+    nee = subk(normalized(0), ee, "KB_16_28", "-EE")
+    inner = mul_sum2(u, tu, e, nee, "U (T - U) - E EE")
+    w3 = norm(shl(mul(w, inner, "w inner"), 3), "W3")
+    z3 = norm(shl(e, 1), "Z3=2E")
+    return x3, w3, z3
+
+
+def ladder_invariant_w(base_x, base_w, rounds=12):
+    """ladder_invariant for the G1 fast ladders (mul_abs_u_affine<fp>) in W = 2Y coordinates,
+    including the opening tripling."""
+    X, W, Z = jac_tpl_affine_w(base_x, base_w)
+
+    def step(X, W, Z):
+        x1, w1, z1 = jac_dbl_w(X, W, Z)
+        x2, w2, z2 = jac_madd_w(x1, w1, z1, base_x, base_w)
+        return vmax(X, x1, x2), vmax(W, w1, w2), vmax(Z, z1, z2)
+
+    for _ in range(rounds):
+        X, W, Z = step(X, W, Z)
+    S = (_inflate1(X, 1.01), _inflate1(W, 1.01), _inflate1(Z, 1.01))
+    for _ in range(40):
+        T = step(*S)
+        if all(_within(Field(False), a, b) for a, b in zip(T, S)):
+            return S
+        S = tuple(_inflate1(vmax(a, b), 1.01) for a, b in zip(T, S))
+    raise BoundError("W-form ladder bound set is not closed")
 
 
 def jac_dbl(F, X, Y, Z):

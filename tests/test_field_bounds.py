@@ -30,6 +30,20 @@ def test_ladders_closed():
     M.jac_eq_affine(F, *S1, base, base)
 
 
+def test_g1_fast_ladders_w_closed():
+    """The G1 fast ladders (curve.hpp in_subgroup_fast_g1: jac_tpl_affine_w / jac_dbl_w /
+    jac_madd_w, W = 2Y): the base's w = 2y (a doubled normalized y), the second ladder's base is
+    Q1 = (X, W) of the first, and the comparison is with (beta x, 2 (-y))."""
+    base = M.normalized(Fraction(101, 100))
+    w = M.shl(base, 1, "2y")
+    S1 = M.ladder_invariant_w(base, w)
+    S2 = M.ladder_invariant_w(S1[0], S1[1])
+    z = M.mul(S2[2], S1[2], "Z'Z")
+    beta_x = M.mul(base, M.normalized(1))
+    nw = M.shl(M.norm(M.subk(M.normalized(0), base, "KB_64_31")), 1, "-2y")
+    M.jac_eq_affine(M.Field(False), S2[0], S2[1], z, beta_x, nw)
+
+
 def _pow_pm3d4(a):
     """fp_pow_pm3d4: table a, a^3, .., a^15 (via a^2), then squarings / table multiplies.
     BLS12-381 runs it on the radix-2^30 core (fp_pow_pm3d4_30, proven in tests/test_fp30.py for any

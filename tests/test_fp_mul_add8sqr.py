@@ -6,6 +6,8 @@ below 2^30 + 2^28, c = B normalized). CPU only; the column bounds for the whole 
 tests/test_field_bounds.py (field_bounds_model.mul_add8sqr)."""
 import random
 
+import pytest
+
 P = 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB153FFFFB9FEFFFFFFFFAAAB
 N, LB = 14, 28
 MASK = (1 << LB) - 1
@@ -20,9 +22,9 @@ def u64(x, what):
     return x
 
 
-def mul_add8sqr(a, b, c):
-    c8 = [x << 3 for x in c]
-    c16 = [x << 4 for x in c]
+def mul_add8sqr(a, b, c, scale=8):
+    c8 = [x * scale for x in c]
+    c16 = [x * 2 * scale for x in c]
     assert all(x < 1 << 32 for x in c16)
     m, r, acc = [0] * N, [0] * N, 0
     for i in range(2 * N):
@@ -58,14 +60,19 @@ def rand_limbs(rng, limb_max, top_max):
     return [rng.randrange(limb_max + 1) for _ in range(N - 1)] + [rng.randrange(top_max + 1)]
 
 
-def test_mul_add8sqr_exact():
-    rng = random.Random(8)
+@pytest.mark.parametrize("scale", [8, 1])
+def test_mul_add8sqr_exact(scale):
+    """scale 8: fp_mul_addsqr<8> (the Y-form doubling); scale 1: fp_mul_addsqr<1> (jac_dbl_w, whose
+    b = 2 (X3 - D) has limbs below 2^31 + 2^29)."""
+    rng = random.Random(8 + scale)
     top_n = (3 * P) >> (LB * (N - 1))          # normalized operands: values below ~3 p
     a_max, b_max = MASK, (1 << 30) + (1 << 28)  # E normalized; F - 3D + KB_8_30 lazy
+    if scale == 1:
+        b_max = 2 * b_max  # doubled
     cases = [([MASK] * (N - 1) + [top_n], [b_max] * (N - 1) + [top_n << 3], [MASK] * (N - 1) + [top_n])]
     for _ in range(400):
         cases.append((rand_limbs(rng, a_max, top_n), rand_limbs(rng, b_max, top_n << 3), rand_limbs(rng, MASK, top_n)))
     for a, b, c in cases:
-        r = mul_add8sqr(a, b, c)
+        r = mul_add8sqr(a, b, c, scale)
         assert all(x <= MASK for x in r)
-        assert (val(r) * R - (val(a) * val(b) + 8 * val(c) ** 2)) % P == 0
+        assert (val(r) * R - (val(a) * val(b) + scale * val(c) ** 2)) % P == 0

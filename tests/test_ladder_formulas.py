@@ -136,6 +136,79 @@ def tpl_g2(x, y):
     return x3, y3, e
 
 
+def dbl_g1_w(X, W, Z):
+    F = Fp
+    a, b = F.sqr(X), F.sqr(W)                       # B' = W^2
+    d = F.mul(X, b)
+    e = F.k(3, a)
+    z3 = F.mul(W, Z)
+    f = F.sqr(e)
+    x3 = F.sub(f, F.k(2, d))
+    nw3 = F.add(F.mul(e, F.k(2, F.sub(x3, d))), F.sqr(b))
+    return x3, F.sub(0, nw3), z3
+
+
+def madd_g1_w(X, W, Z, x2, w2):
+    F = Fp
+    if Z == 0:
+        return x2, w2, 1
+    z1z1 = F.sqr(Z)
+    h = F.sub(F.mul(x2, z1z1), X)
+    r = F.sub(F.mul(F.mul(w2, Z), z1z1), W)         # 2 S2 - W1 = ark's r
+    if h == 0 and r == 0:
+        return dbl_g1_w(X, W, Z)
+    hh = F.sqr(h)
+    z3 = F.mul(F.k(2, Z), h)
+    i = F.k(4, hh)
+    j = F.mul(h, i)
+    v = F.mul(X, i)
+    x3 = F.sub(F.sub(F.sqr(r), j), F.k(2, v))
+    w3 = F.sub(F.mul(F.k(2, r), F.sub(v, x3)), F.mul(F.k(2, W), j))
+    return x3, w3, z3
+
+
+def tpl_g1_w(x, w):
+    F = Fp
+    xx, yyw = F.sqr(x), F.sqr(w)
+    t = F.sqr(yyw)
+    m = F.k(3, xx)
+    mm = F.sqr(m)
+    e = F.sub(F.k(3, F.mul(x, yyw)), mm)
+    ee = F.sqr(e)
+    u = F.sub(F.sub(F.sub(F.sqr(F.add(m, e)), mm), ee), t)
+    x3 = F.k(4, F.sub(F.mul(x, ee), F.mul(yyw, u)))
+    w3 = F.k(8, F.mul(w, F.sub(F.mul(u, F.sub(t, u)), F.mul(e, ee))))
+    return x3, w3, F.k(2, e)
+
+
+def mul_abs_u_w(bw):
+    """mul_abs_u_affine<fp>: the W = 2Y ladder from the base (x, w = 2y); returns (X, W, Z)."""
+    X, W, Z = tpl_g1_w(*bw)
+    for b in range(ABS_U.bit_length() - 3, -1, -1):
+        X, W, Z = dbl_g1_w(X, W, Z)
+        if (ABS_U >> b) & 1:
+            X, W, Z = madd_g1_w(X, W, Z, *bw)
+    return X, W, Z
+
+
+def test_g1_w_form_ladders():
+    """in_subgroup_fast_g1's W = 2Y ladders: [|u|] P, then [|u|] of Q1 = (X, W) on the isomorphic
+    curve (its base w is Q1's W), compared with (beta x, 2 (-y)) in W form."""
+    rng = random.Random(6)
+    for pt in _points("g1", rng):
+        X, W, Z = mul_abs_u_w((pt[0], 2 * pt[1] % P))
+        want = O.g1_mul(pt, ABS_U)
+        got = None if Z == 0 else (X * pow(Z * Z, P - 2, P) % P, W * pow(2 * Z ** 3, P - 2, P) % P)
+        assert got == want, pt
+        if Z == 0:
+            continue
+        # second ladder: base (X, W) is (x, 2y) of the affine point (X, W / 2) on E'
+        X2, W2, Z2 = mul_abs_u_w((X, W))
+        z = Z2 * Z % P
+        got2 = (X2 * pow(z * z, P - 2, P) % P, W2 * pow(2 * z ** 3, P - 2, P) % P)
+        assert got2 == O.g1_mul(pt, ABS_U * ABS_U), pt
+
+
 def mul_abs_u_jac(F, dbl, tpl, base):
     X, Y, Z = tpl(*base)
     for b in range(ABS_U.bit_length() - 3, -1, -1):
