@@ -413,6 +413,127 @@ KZG_DEV void jac_madd(jac<fp2>& p, Load&& load) {
   p.x = t;
 }
 
+// ---------------------------------------------------------------- G2 fast ladder, W = 2Y
+// As the G1 W form (jac_dbl_w above): B' = W^2, D = X B' and Z3 = W Z need no 4X / 2Y, and
+// W3 = (2E)(D - X3) - B'^2 needs no -8 scaling of B^2's factors; the mixed addition's
+// r = 2 S2 - W1 is ark's r. W limbs reach 2^29 (the base's w = 2y), so the constants borrowed
+// against W are KB_*_29. Bounds: tests/field_bounds_model.py jac_dbl_fp2_w / jac_madd_fp2_w /
+// jac_tpl_affine_fp2_w / ladder_invariant_fp2_w.
+KZG_DEV void jac_dbl_w(jac<fp2>& p) {
+  fp2 b, a, d, t;
+  f2_sqr_lz<BlsFp::KB_32_29>(b, p.y);        // B' = W^2
+  f2_mul_lz<BlsFp::KB_16_28>(p.z, p.y, p.z); // Z3 = W Z           (W dead)
+  f2_sqr_lz<BlsFp::KB_16_28>(a, p.x);        // A = X^2
+  f2_mul_lz<BlsFp::KB_2_28>(d, p.x, b);      // D = X B'           (X dead)
+  fp_mul3_nr(a.c0, a.c0);
+  fp_mul3_nr(a.c1, a.c1);
+  f2_norm(a, a);                             // E = 3 A            (A dead)
+  f2_sqr_lz<BlsFp::KB_4_28>(t, a);           // F = E^2
+  f2_shl<1>(p.x, d);
+  f2_subk<BlsFp::KB_4_29>(p.x, t, p.x);
+  f2_norm(p.x, p.x);                         // X3 = F - 2D        (F dead)
+  f2_subk<BlsFp::KB_8_28>(d, d, p.x);        // t = D - X3
+  f2_shl<1>(a, a);                           // 2E
+  fp u, s, n, c0;
+  fp_negk_nr<BlsFp::KB_16_30>(u, d.c1);      // -t1
+  fp_add_nr(s, b.c0, b.c1);                  // b0 + b1             < 2^29
+  fp_subk_nr<BlsFp::KB_2_28>(n, b.c1, b.c0);
+  fp_norm(n, n);                             // b1 - b0             N
+  fp_mul_sum3(c0, a.c0, d.c0, a.c1, u, s, n);
+  fp_negk_nr<BlsFp::KB_2_28>(n, b.c1);       // -b1                 < 2^29
+  fp_shl_nr<1>(s, b.c0);                     // 2 b0                < 2^29
+  fp_mul_sum3(p.y.c1, a.c0, d.c1, a.c1, d.c0, s, n);
+  p.y.c0 = c0;                               // W3 = 2E (D - X3) - B'^2
+}
+
+// The scaled triple (X3/4, W3/8, E) of 3P from (x, w = 2y): YYw = w^2, T = YYw^2, E = 3 x YYw - MM,
+// X3/4 = x EE - YYw U, W3/8 = w (U (T - U) - E EE). load delivers (x, w); fetched twice.
+template <typename Load>
+KZG_DEV void jac_tpl_affine_w(jac<fp2>& p, Load&& load) {
+  fp2 yy, m, s, ee, t;
+  load(p.x, p.y);
+  f2_sqr_lz<BlsFp::KB_2_28>(m, p.x);         // XX
+  f2_sqr_lz<BlsFp::KB_4_29>(yy, p.y);        // YYw = w^2
+  f2_mul_lz<BlsFp::KB_2_28>(p.z, p.x, yy);   // x YYw               (x, w dead)
+  fp_mul3_nr(m.c0, m.c0);
+  fp_mul3_nr(m.c1, m.c1);
+  f2_norm(m, m);                             // M = 3 XX
+  f2_sqr_lz<BlsFp::KB_4_28>(t, m);           // MM
+  fp_mul3_nr(p.z.c0, p.z.c0);
+  fp_mul3_nr(p.z.c1, p.z.c1);
+  f2_subk<BlsFp::KB_2_28>(p.z, p.z, t);
+  f2_norm(p.z, p.z);                         // E = 3 x YYw - MM = Z3
+  f2_add_nr(s, m, p.z);
+  f2_norm(s, s);
+  f2_sqr_lz<BlsFp::KB_32_28>(s, s);          // S2 = (M + E)^2
+  f2_subk<BlsFp::KB_2_28>(s, s, t);          // - MM
+  f2_sqr_lz<BlsFp::KB_16_28>(ee, p.z);       // EE
+  f2_subk<BlsFp::KB_4_28>(s, s, ee);         // - EE
+  f2_sqr_lz<BlsFp::KB_2_28>(t, yy);          // T = YYw^2 = 16 YYYY
+  f2_subk<BlsFp::KB_2_28>(s, s, t);
+  f2_norm(s, s);                             // U = S2 - MM - EE - T
+  f2_subk<BlsFp::KB_64_28>(t, t, s);
+  f2_norm(t, t);                             // T - U
+  f2_mul_lz<BlsFp::KB_128_28>(t, s, t);      // U (T - U)
+  f2_mul_lz<BlsFp::KB_64_28>(yy, yy, s);     // YYw U
+  f2_mul_lz<BlsFp::KB_2_28>(m, p.z, ee);     // E EE
+  f2_subk<BlsFp::KB_2_28>(t, t, m);
+  f2_norm(t, t);                             // U (T - U) - E EE
+  load(p.x, p.y);
+  f2_mul_lz<BlsFp::KB_2_28>(p.x, p.x, ee);   // x EE
+  f2_subk<BlsFp::KB_2_28>(p.x, p.x, yy);
+  f2_norm(p.x, p.x);                         // X3 / 4 = x EE - YYw U
+  f2_mul_lz<BlsFp::KB_8_28>(p.y, p.y, t);    // W3 / 8 = w (U (T - U) - E EE)
+}
+
+template <typename Load>
+KZG_DEV void jac_madd_w(jac<fp2>& p, Load&& load) {
+  fp2 z1z1, h, r, t;
+  {
+    fp2 x2, w2;
+    load(x2, w2);
+    f2_sqr_lz<BlsFp::KB_16_28>(z1z1, p.z);
+    f2_mul_lz<BlsFp::KB_2_28>(h, x2, z1z1);  // U2
+    f2_subk<BlsFp::KB_32_28>(h, h, p.x);
+    f2_norm(h, h);                           // H = U2 - X1
+    f2_mul_lz<BlsFp::KB_16_28>(t, w2, p.z);
+    f2_mul_lz<BlsFp::KB_2_28>(t, t, z1z1);   // 2 S2
+    f2_subk<BlsFp::KB_32_29>(r, t, p.y);
+    f2_norm(r, r);                           // r = 2 S2 - W1 = 2 (S2 - Y1)
+  }
+  const bool z1zero = f_is_zero(p.z);
+  const bool same = !z1zero && f_is_zero(h) && f_is_zero(r);
+  if (__builtin_expect(z1zero || same, 0)) {
+    if (same) {
+      jac_dbl_w(p);
+    } else {
+      load(p.x, p.y);
+      f_one(p.z);
+    }
+    return;
+  }
+  fp2 hh, j;
+  f2_sqr_lz<BlsFp::KB_64_28>(hh, h);         // HH
+  f2_shl<1>(t, p.z);
+  f2_mul_lz<BlsFp::KB_64_28>(p.z, t, h);     // Z3 = 2 Z1 H
+  f2_shl<2>(hh, hh);                         // I = 4 HH
+  f2_mul_lz<BlsFp::KB_8_30>(j, h, hh);       // J = H I
+  f2_mul_lz<BlsFp::KB_8_30>(hh, p.x, hh);    // V = X1 I
+  f2_sqr_lz<BlsFp::KB_64_28>(t, r);          // r^2
+  f2_subk<BlsFp::KB_2_28>(t, t, j);
+  f2_shl<1>(h, hh);                          // 2V
+  f2_subk<BlsFp::KB_4_29>(t, t, h);
+  f2_norm(t, t);                             // X3 = r^2 - J - 2V
+  f2_subk<BlsFp::KB_32_28>(hh, hh, t);       // V - X3
+  f2_shl<1>(r, r);                           // 2r
+  f2_mul_lz<BlsFp::KB_64_30>(hh, r, hh);     // 2r (V - X3)
+  f2_shl<1>(h, p.y);                         // 2 W1
+  f2_mul_lz<BlsFp::KB_2_28>(j, h, j);        // 2 W1 J
+  f2_subk<BlsFp::KB_4_28>(p.y, hh, j);
+  f2_norm(p.y, p.y);                         // W3 = 2r (V - X3) - 2 W1 J
+  p.x = t;
+}
+
 // ---------------------------------------------------------------- mixed addition (cold)
 // ark add_assign_mixed: p += (x2, y2) for a finite affine (x2, y2) that `load(x2, y2)` delivers
 // (normalized, v <= 2 — or, for the G1 test's second ladder, a ladder state: limbs < 2^30). The
@@ -481,12 +602,16 @@ KZG_DEV void mul_abs_u_affine(jac<F>& acc, Load&& load) {
       jac_dbl_w(acc);
       if ((BLS_ABS_U >> b) & 1) jac_madd_w(acc, load);
     }
-  } else {
-    jac_tpl_affine(acc, load);
+  } else {  // W = 2Y form as well: load delivers (x, y), doubled here
+    auto loadw = [&](fp2& x, fp2& w) {
+      load(x, w);
+      f2_shl<1>(w, w);
+    };
+    jac_tpl_affine_w(acc, loadw);
 #pragma unroll 1
     for (int b = BLS_ABS_U_BITS - 3; b >= 0; b--) {
-      jac_dbl(acc);
-      if ((BLS_ABS_U >> b) & 1) jac_madd(acc, load);
+      jac_dbl_w(acc);
+      if ((BLS_ABS_U >> b) & 1) jac_madd_w(acc, loadw);
     }
   }
 }
@@ -514,7 +639,7 @@ KZG_DEV bool jac_eq_affine(const jac<fp2>& p, const fp2& x, const fp2& y) {
   bool ok = f_is_zero(t);
   f2_mul_lz<BlsFp::KB_16_28>(z2, z2, p.z);
   f2_mul_lz<BlsFp::KB_2_28>(t, y, z2);
-  f2_subk<BlsFp::KB_32_28>(t, t, p.y);
+  f2_subk<BlsFp::KB_32_29>(t, t, p.y);      // the fast ladder's W limbs reach 2^29
   ok = ok && f_is_zero(t);
   return ok && !f_is_zero(p.z);
 }
@@ -598,6 +723,7 @@ KZG_DEV bool in_subgroup_fast_g2(Load&& load) {
   load(x, y);
   g2_psi(x, y);
   fp2_neg_red(y, y);
+  f2_shl<1>(y, y);  // the ladder carries W = 2Y: compare with 2 (-psi(P).y)
   return jac_eq_affine(q, x, y);
 }
 

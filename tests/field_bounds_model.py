@@ -694,7 +694,7 @@ def jac_eq_affine_fp2_lz(X, Y, Z, x, y):
     t = subk2(mul2(x, z2, "KB_2_28", "xZ2"), X, "KB_32_28", "eqx")
     zero_ok2(t, "eqx")
     z3 = mul2(z2, Z, "KB_16_28", "z3")
-    t = subk2(mul2(y, z3, "KB_2_28", "yZ3"), Y, "KB_32_28", "eqy")
+    t = subk2(mul2(y, z3, "KB_2_28", "yZ3"), Y, "KB_32_29", "eqy")
     zero_ok2(t, "eqy")
     zero_ok2(Z, "Z")
 
@@ -731,3 +731,105 @@ def ladder_invariant_fp2_lz(base_x, base_y, rounds=12):
             return S
         S = tuple(infl(join2(a, b)) for a, b in zip(T, S))
     raise BoundError("lazy Fp2 ladder bound set is not closed")
+
+
+# ---- the G2 fast ladder in W = 2Y coordinates (curve.hpp jac_dbl_w / jac_madd_w / jac_tpl_affine_w
+# over Fp2): the same savings as the G1 W form
+def jac_dbl_fp2_w(X, W, Z):
+    """jac_dbl_w(jac<fp2>&): B' = W^2, Z3 = W Z, D = X B', E = 3A, X3 = F - 2D, t = D - X3,
+    W3 = (2E) t - B'^2 as two three-product sums per component."""
+    b = sqr2(W, "KB_32_29", "B'")
+    z3 = mul2(W, Z, "KB_16_28", "Z3")
+    a = sqr2(X, "KB_16_28", "A")
+    d = mul2(X, b, "KB_2_28", "D")
+    e = norm2(mul3_2(a), "E")
+    f = sqr2(e, "KB_4_28", "F")
+    x3 = norm2(subk2(f, shl2(d, 1), "KB_4_29", "X3"), "X3")
+    t = subk2(d, x3, "KB_8_28", "D-X3")
+    e2 = shl2(e, 1, "2E")
+    u = subk(normalized(0), t.c1, "KB_16_30", "-t1")
+    s = add_nr(b.c0, b.c1, "b0+b1")
+    n0 = norm(subk(b.c1, b.c0, "KB_2_28", "b1-b0"), "b1-b0")
+    w0 = mul_sum3(e2.c0, t.c0, e2.c1, u, s, n0, "W3.c0")
+    n1 = subk(normalized(0), b.c1, "KB_2_28", "-b1")
+    w1 = mul_sum3(e2.c0, t.c1, e2.c1, t.c0, shl(b.c0, 1), n1, "W3.c1")
+    return x3, V2(w0, w1), z3
+
+
+def jac_tpl_affine_fp2_w(x, w):
+    """jac_tpl_affine_w(jac<fp2>&): the scaled triple (X3/4, W3/8, E) from (x, w = 2y):
+    YYw = w^2, T = YYw^2, E = 3 x YYw - MM, X3/4 = x EE - YYw U, W3/8 = w (U (T - U) - E EE)."""
+    xx = sqr2(x, "KB_2_28", "XX")
+    yyw = sqr2(w, "KB_4_29", "YYw")
+    t = sqr2(yyw, "KB_2_28", "T")
+    m = norm2(mul3_2(xx), "M")
+    mm = sqr2(m, "KB_4_28", "MM")
+    e = norm2(subk2(mul3_2(mul2(x, yyw, "KB_2_28", "x YYw")), mm, "KB_2_28", "3 x YYw - MM"), "E")
+    ee = sqr2(e, "KB_16_28", "EE")
+    s2 = sqr2(norm2(add2(m, e), "M+E"), "KB_32_28", "S2")
+    u = subk2(subk2(subk2(s2, mm, "KB_2_28", "S2-MM"), ee, "KB_4_28", "-EE"), t, "KB_2_28", "-T")
+    u = norm2(u, "U")
+    a = mul2(x, ee, "KB_2_28", "xEE")
+    b = mul2(yyw, u, "KB_64_28", "YYwU")
+    x3 = norm2(subk2(a, b, "KB_2_28", "xEE-YYwU"), "X3/4")
+    c = mul2(u, norm2(subk2(t, u, "KB_64_28", "T-U"), "T-U"), "KB_128_28", "U(T-U)")
+    d = mul2(e, ee, "KB_2_28", "E EE")
+    inner = norm2(subk2(c, d, "KB_2_28", "inner"), "inner")
+    w3 = mul2(w, inner, "KB_8_28", "W3/8")
+    return x3, w3, e
+
+
+def jac_madd_fp2_w(X, W, Z, x2, w2):
+    """jac_madd_w(jac<fp2>&): r = 2 S2 - W1, X3 = r^2 - J - 2V, W3 = 2r (V - X3) - 2 W1 J."""
+    z1z1 = sqr2(Z, "KB_16_28", "Z1Z1")
+    u2 = mul2(x2, z1z1, "KB_2_28", "U2")
+    h = norm2(subk2(u2, X, "KB_32_28", "H"), "H")
+    t = mul2(w2, Z, "KB_16_28", "w2Z")
+    s2 = mul2(t, z1z1, "KB_2_28", "2S2")
+    r = norm2(subk2(s2, W, "KB_32_29", "r"), "r")
+    zero_ok2(Z, "Z"), zero_ok2(h, "H"), zero_ok2(r, "r")
+    xd, wd, zd = jac_dbl_fp2_w(X, W, Z)
+    hh = sqr2(h, "KB_64_28", "HH")
+    z3 = mul2(shl2(Z, 1), h, "KB_64_28", "Z3m")
+    i = shl2(hh, 2, "I")
+    j = mul2(h, i, "KB_8_30", "J")
+    v = mul2(X, i, "KB_8_30", "V")
+    rr = sqr2(r, "KB_64_28", "r^2")
+    x3 = subk2(rr, j, "KB_2_28", "X3a")
+    x3 = norm2(subk2(x3, shl2(v, 1), "KB_4_29", "X3m"), "X3m")
+    vx = subk2(v, x3, "KB_32_28", "V-X3")
+    a = mul2(shl2(r, 1), vx, "KB_64_30", "2r(V-X3)")
+    b = mul2(shl2(W, 1), j, "KB_2_28", "2W1J")
+    w3 = norm2(subk2(a, b, "KB_4_28", "W3m"), "W3m")
+    return (V2(vmax(x3.c0, xd.c0, x2.c0), vmax(x3.c1, xd.c1, x2.c1)),
+            V2(vmax(w3.c0, wd.c0, w2.c0), vmax(w3.c1, wd.c1, w2.c1)),
+            V2(vmax(z3.c0, zd.c0, normalized(1)), vmax(z3.c1, zd.c1, normalized(1))))
+
+
+def ladder_invariant_fp2_w(base_x, base_w, rounds=12):
+    """ladder_invariant for the G2 fast ladder in W form (mul_abs_u_affine<fp2>)."""
+    def join2(a, b):
+        return V2(vmax(a.c0, b.c0), vmax(a.c1, b.c1))
+
+    def infl(a):
+        return V2(_inflate1(a.c0, 1.01), _inflate1(a.c1, 1.01))
+
+    def within(a, b):
+        return all(all(x <= y for x, y in zip(u.limbs, w.limbs)) and u.val <= w.val
+                   for u, w in ((a.c0, b.c0), (a.c1, b.c1)))
+
+    def step(X, W, Z):
+        x1, w1, z1 = jac_dbl_fp2_w(X, W, Z)
+        x2, w2, z2 = jac_madd_fp2_w(x1, w1, z1, base_x, base_w)
+        return join2(join2(X, x1), x2), join2(join2(W, w1), w2), join2(join2(Z, z1), z2)
+
+    X, W, Z = jac_tpl_affine_fp2_w(base_x, base_w)
+    for _ in range(rounds):
+        X, W, Z = step(X, W, Z)
+    S = (infl(X), infl(W), infl(Z))
+    for _ in range(40):
+        T = step(*S)
+        if all(within(a, b) for a, b in zip(T, S)):
+            return S
+        S = tuple(infl(join2(a, b)) for a, b in zip(T, S))
+    raise BoundError("W-form Fp2 ladder bound set is not closed")

@@ -124,6 +124,16 @@ def test_g2_lazy_ladder_closed():
     M.jac_eq_affine_fp2_lz(*S, red, red)
 
 
+def test_g2_fast_ladder_w_closed():
+    """The G2 fast ladder (in_subgroup_fast_g2) in W = 2Y form: base (x, 2y), compared with
+    (x', 2 y') for psi's output (x', y') reduced."""
+    base = M.V2(M.normalized(Fraction(101, 100)), M.normalized(Fraction(101, 100)))
+    w = M.V2(M.shl(base.c0, 1), M.shl(base.c1, 1))
+    S = M.ladder_invariant_fp2_w(base, w)
+    red = M.V2(M.reduced(), M.reduced())
+    M.jac_eq_affine_fp2_lz(*S, red, M.V2(M.shl(red.c0, 1), M.shl(red.c1, 1)))
+
+
 def test_g2_synth_madd_chain_lazy():
     """k_synth<fp2> (synth_kernels.hip): back-to-back lazy Fp2 mixed additions of table points,
     then to_affine's reduced-discipline inverse and multiplies (inputs normalized, any value)."""

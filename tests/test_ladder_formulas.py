@@ -278,3 +278,70 @@ def test_g1_second_ladder_on_isomorphic_curve():
             # on G1, [u^2] P = (beta x, -y) for one of the two primitive cube roots of unity beta
             b = next(c for c in (pow(g, (P - 1) // 3, P) for g in range(2, 20)) if c != 1)
             assert got in [((b * pt[0]) % P, (-pt[1]) % P), ((b * b * pt[0]) % P, (-pt[1]) % P)]
+
+
+def dbl_g2_w(X, W, Z):
+    F = Fp2
+    b = F.sqr(W)
+    z3 = F.mul(W, Z)
+    d = F.mul(X, b)
+    e = F.k(3, F.sqr(X))
+    x3 = F.sub(F.sqr(e), F.k(2, d))
+    t = F.sub(d, x3)
+    (e0, e1), (t0, t1), (b0, b1) = F.k(2, e), t, b
+    w0 = (e0 * t0 + e1 * (-t1) + (b0 + b1) * (b1 - b0)) % P
+    w1 = (e0 * t1 + e1 * t0 + (2 * b0) * (-b1)) % P
+    return x3, (w0, w1), z3
+
+
+def madd_g2_w(X, W, Z, x2, w2):
+    F = Fp2
+    if Z == F.zero:
+        return x2, w2, F.one
+    z1z1 = F.sqr(Z)
+    h = F.sub(F.mul(x2, z1z1), X)
+    r = F.sub(F.mul(F.mul(w2, Z), z1z1), W)
+    if h == F.zero and r == F.zero:
+        return dbl_g2_w(X, W, Z)
+    hh = F.sqr(h)
+    z3 = F.mul(F.k(2, Z), h)
+    i = F.k(4, hh)
+    j = F.mul(h, i)
+    v = F.mul(X, i)
+    x3 = F.sub(F.sub(F.sqr(r), j), F.k(2, v))
+    w3 = F.sub(F.mul(F.k(2, r), F.sub(v, x3)), F.mul(F.k(2, W), j))
+    return x3, w3, z3
+
+
+def tpl_g2_w(x, w):
+    F = Fp2
+    xx, yyw = F.sqr(x), F.sqr(w)
+    t = F.sqr(yyw)
+    m = F.k(3, xx)
+    mm = F.sqr(m)
+    e = F.sub(F.k(3, F.mul(x, yyw)), mm)
+    ee = F.sqr(e)
+    u = F.sub(F.sub(F.sub(F.sqr(F.add(m, e)), mm), ee), t)
+    x3 = F.sub(F.mul(x, ee), F.mul(yyw, u))
+    w3 = F.mul(w, F.sub(F.mul(u, F.sub(t, u)), F.mul(e, ee)))
+    return x3, w3, e
+
+
+def test_g2_w_form_ladder():
+    """mul_abs_u_affine<fp2> in W = 2Y form: the W result over 2 Z^3 is [|u|] P's y."""
+    rng = random.Random(7)
+    for pt in _points("g2", rng):
+        bw = (pt[0], Fp2.k(2, pt[1]))
+        X, W, Z = tpl_g2_w(*bw)
+        for b in range(ABS_U.bit_length() - 3, -1, -1):
+            X, W, Z = dbl_g2_w(X, W, Z)
+            if (ABS_U >> b) & 1:
+                X, W, Z = madd_g2_w(X, W, Z, *bw)
+        want = O.g2_mul(pt, ABS_U)
+        if Z == Fp2.zero:
+            assert want is None
+            continue
+        zi = Fp2.inv(Z)
+        zi2 = Fp2.sqr(zi)
+        got = (Fp2.mul(X, zi2), Fp2.mul(Fp2.mul(W, zi2), Fp2.mul(zi, (pow(2, P - 2, P), 0))))
+        assert got == want, pt
