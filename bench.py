@@ -12,6 +12,11 @@ arkworks buffer on every rank (strong scaling: the transcript is fixed, ranks sp
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
+`--gpus N > 1` without a launcher starts `torch.distributed.run` itself, as a CHILD process,
+before anything touches the GPU, forwards rank 0's JSON line and exits with the child's code;
+under a launcher, WORLD_SIZE != --gpus is an error. The line carries RCCL's own view of the
+communicator (`rccl_nranks`, per-rank devices) so an N-GPU number is proven to be one.
+
 Prints ONE JSON line (rank 0). `roofline` is for the dominant kernel pair (G1 decompress + G1
 check), timed with HIP events on the launch stream; `valu` prices the same launches against the
 cycle-weighted integer-VALU issue roof (profiles/r02_valu_mix.json); `cpu_baseline` times the C
@@ -75,6 +80,8 @@ def parse():
     ap.add_argument("--no-next-rows", action="store_true", help="skip the SURVEY 8f rows and config 5")
     ap.add_argument("--bn254-log2", type=int, default=28, help="config 5 size (0 = skip)")
     ap.add_argument("--e2e-log2", type=int, default=21, help="end-to-end preprocess N (0 = skip)")
+    ap.add_argument("--no-host-api", dest="host_api", action="store_false",
+                    help="skip the host-buffer FFI rows (next_rows.host_api)")
     return ap.parse_args()
 
 
@@ -452,7 +459,58 @@ def oracle_sample_check(stream, runs):
             "equal": bool(ok), "seconds": time.perf_counter() - t}
 
 
-def e2e_preprocess(n_log2, seed, dev, kzgpot, D):
+def host_api_rows(seed, dev, D, g1_log2=25, g2_log2=20):
+    """The FFI boundary the Rust caller binds (include/kzgpot.h): kzgpot_g1_decompress /
+    kzgpot_g2_decompress on PAGEABLE host buffers, as `read_g1` x N is replaced
+    (src/lib.rs:41-80, preprocess-kgz.rs:140-153), timed around the C call: PCIe both ways
+    included (run_host pipelines 2^21-point chunks over two streams). Beside each, the same points
+    device-resident (the `_dev` launch, event-timed), so the PCIe overhead is explicit. The first
+    call sizes the staging and faults the output pages in; the steady-state call is the row."""
+    import numpy as np
+    import torch
+    from kzgpot import _lib
+    from kzgpot import dist as KD
+
+    lib = _lib.load()
+    rows = {}
+    for kind, lg, fn, rout in (("g1", g1_log2, lib.kzgpot_g1_decompress, 96),
+                               ("g2", g2_log2, lib.kzgpot_g2_decompress, 192)):
+        n = 1 << lg
+        comp, exp = D.synth(kind, seed, 0, n, dev, with_expected=True)
+        host_in = comp.cpu().numpy()
+        want = exp.cpu().numpy()
+        out = np.empty(n * rout, np.uint8)  # pageable, as a Rust Vec<u8>
+        fb = ctypes.c_int64()
+        t = time.perf_counter()
+        rc0 = fn(host_in.ctypes.data, ctypes.c_size_t(n), out.ctypes.data, 0, ctypes.byref(fb))
+        first_s = time.perf_counter() - t
+        out[:] = 0
+        t = time.perf_counter()
+        rc = fn(host_in.ctypes.data, ctypes.c_size_t(n), out.ctypes.data, 0, ctypes.byref(fb))
+        host_s = time.perf_counter() - t
+        ok = rc0 == 0 and rc == 0 and fb.value == -1 and np.array_equal(out, want)
+        d_out = torch.empty(n * rout, dtype=torch.uint8, device=dev)
+        key = torch.empty(1, dtype=torch.int64, device=dev)
+        D.codec_dev(f"{kind}_decompress", comp, d_out, key)
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        e[0].record()
+        D.codec_dev(f"{kind}_decompress", comp, d_out, key)
+        e[1].record()
+        torch.cuda.synchronize()
+        dev_s = e[0].elapsed_time(e[1]) * 1e-3
+        ok = ok and D.read_key(key) == KD.NO_BAD and torch.equal(d_out, exp)
+        rows[f"{kind}_decompress"] = {
+            "entry_point": f"kzgpot_{kind}_decompress (pageable host in/out, synchronous)",
+            "points": n, "seconds": host_s, "points_per_s": n / host_s,
+            "device_resident_s": dev_s, "device_resident_points_per_s": n / dev_s,
+            "pcie_overhead_frac": host_s / dev_s - 1,
+            "pcie_bytes": n * (rout + rout // 2), "first_call_s": first_s, "verified_bit_exact": bool(ok)}
+        del comp, exp, d_out, host_in, want, out
+        torch.cuda.empty_cache()
+    return rows
+
+
+def e2e_preprocess(n_log2, seed, dev, kzgpot, D, n_gpus=1):
     """Build a synthetic response transcript (powersoftau layout, GPU-generated valid points) and
     time the C ABI end to end in both modes: kzgpot_preprocess_buffer_ex (host buffers in and
     out, the output buffer pre-faulted; the Python wrapper's extra copies are not the product)
@@ -494,26 +552,40 @@ def e2e_preprocess(n_log2, seed, dev, kzgpot, D):
     for mode, name in ((kzgpot.MODE_KZG, "preprocess_kgz_e2e"), (kzgpot.MODE_FASTKZG, "preprocess_fastkgz_e2e")):
         size = kzgpot.output_size(n_log2, mode)
         sec, idx = ctypes.c_int(-1), ctypes.c_int64(-1)
+        # the GPU + PCIe part alone: the same call without the two BLAKE2b digests
+        t0 = time.perf_counter()
+        r0 = lib.kzgpot_preprocess_buffer_ex(tr.ctypes.data, tr.size, out.ctypes.data, mode, n_log2, n_gpus, None,
+                                             None, None, ctypes.byref(sec), ctypes.byref(idx))
+        dt0 = time.perf_counter() - t0
+        g1n = (2 * n - 1) * 96
+        ok0 = r0 == 0 and np.array_equal(out[:g1n], expect["tau_g1"]) and \
+            np.array_equal(out[g1n:g1n + n * 96], expect["alpha_g1"])
+        pts = (2 * n - 1) + 3 * n + 1
+        rows[name.replace("_e2e", "_buffer_no_digest")] = {
+            "workload": f"N = 2^{n_log2} response transcript -> {size} B output, host buffers, {n_gpus} shard(s) "
+                        "over the visible GPUs, NO digests: decode + check + PCIe only (C ABI call timed)",
+            "seconds": dt0, "points": pts, "points_per_s": pts / dt0, "n_gpus": n_gpus,
+            "sections_verified": bool(ok0)}
+        out[:] = 1
         din, dout = ctypes.create_string_buffer(129), ctypes.create_string_buffer(129)
         t0 = time.perf_counter()
-        r = lib.kzgpot_preprocess_buffer_ex(tr.ctypes.data, tr.size, out.ctypes.data, mode, n_log2, 1, None, din,
+        r = lib.kzgpot_preprocess_buffer_ex(tr.ctypes.data, tr.size, out.ctypes.data, mode, n_log2, n_gpus, None, din,
                                             dout, ctypes.byref(sec), ctypes.byref(idx))
         dt = time.perf_counter() - t0
-        g1n = (2 * n - 1) * 96
         ok = r == 0 and np.array_equal(out[:g1n], expect["tau_g1"]) and \
             np.array_equal(out[g1n:g1n + n * 96], expect["alpha_g1"])
         buf_digest = hashlib.blake2b(out[:size]).hexdigest()
         ok = ok and din.value.decode() == tr_digest and dout.value.decode() == buf_digest
-        pts = (2 * n - 1) + 3 * n + 1
         rows[name] = {"workload": f"N = 2^{n_log2} response transcript ({tr.size} B) -> {size} B file, "
-                                  "host buffers, 1 GPU, BLAKE2b of input and output (C ABI call timed)",
-                      "seconds": dt, "points": pts, "points_per_s": pts / dt, "sections_verified": bool(ok),
+                                  f"host buffers, {n_gpus} shard(s), BLAKE2b of input and output (C ABI call timed)",
+                      "seconds": dt, "points": pts, "points_per_s": pts / dt, "n_gpus": n_gpus,
+                      "sections_verified": bool(ok),
                       "transcript_blake2b": din.value.decode()[:16] + "...",
                       "output_blake2b": dout.value.decode()[:16] + "..."}
         # file to file (the reference's contract, preprocess-kgz.rs:69-126,187-194)
         dst = os.path.join(tmpdir, "out")
         t0 = time.perf_counter()
-        r = lib.kzgpot_preprocess_ex(src.encode(), dst.encode(), mode, n_log2, 1, None, din, dout,
+        r = lib.kzgpot_preprocess_ex(src.encode(), dst.encode(), mode, n_log2, n_gpus, None, din, dout,
                                      ctypes.byref(sec), ctypes.byref(idx))
         dtf = time.perf_counter() - t0
         with open(dst, "rb") as f:
@@ -522,7 +594,8 @@ def e2e_preprocess(n_log2, seed, dev, kzgpot, D):
         rows[name + "_file"] = {
             "workload": f"same, file to file: kzgpot_preprocess_ex({tr.size} B transcript on local disk -> output "
                         "file), transcript pread() behind the GPU, output pwrite() behind it, both digests",
-            "seconds": dtf, "points_per_s": pts / dtf, "buffer_path_s": dt, "transcript_read_s": read_s,
+            "seconds": dtf, "points_per_s": pts / dtf, "n_gpus": n_gpus, "buffer_path_s": dt,
+            "transcript_read_s": read_s,
             "vs_buffer_plus_read": dtf / (dt + read_s),
             "file_verified": bool(r == 0 and file_digest == buf_digest == dout.value.decode())}
     os.unlink(src)
@@ -530,8 +603,70 @@ def e2e_preprocess(n_log2, seed, dev, kzgpot, D):
     return rows
 
 
+def spawn_ranks(args) -> int:
+    """`bench.py --gpus N` (N > 1) with no launcher around it: run `torch.distributed.run
+    --nproc-per-node N ... bench.py <same args>` as a child process (never exec: this process has
+    not touched the GPU, and must not), pass rank 0's JSON line through to stdout, everything else
+    to stderr, and return the child's exit code."""
+    import socket
+    import subprocess
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:  # a free rendezvous port
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = spawn_argv(args.gpus, port, sys.argv[1:])
+    env = dict(os.environ, KZGPOT_BENCH_LAUNCHER="bench.py -> torch.distributed.run (child process)")
+    print(f"bench.py: --gpus {args.gpus}: starting {' '.join(cmd)}", file=sys.stderr, flush=True)
+    p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True)
+    for line in p.stdout:
+        if line.startswith("{") and '"metric"' in line:
+            sys.stdout.write(line)
+            sys.stdout.flush()
+        else:
+            sys.stderr.write(line)
+    return p.wait()
+
+
+def spawn_argv(n, port, argv):
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def check_launch(gpus, environ):
+    """None if this process may run the bench itself, 'spawn' if it must start the ranks, or an
+    error message (a launcher whose WORLD_SIZE disagrees with --gpus)."""
+    if "WORLD_SIZE" in environ:
+        world = int(environ["WORLD_SIZE"])
+        if world != gpus:
+            return f"--gpus {gpus} but the launcher started WORLD_SIZE {world} ranks"
+        return None
+    return "spawn" if gpus > 1 else None
+
+
+def rank_info(dev, comm):
+    """This rank's device as torch and (when the library communicator exists) as RCCL sees it."""
+    import socket
+
+    import torch
+
+    props = torch.cuda.get_device_properties(dev)
+    info = {"rank": int(os.environ.get("RANK", "0")), "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
+            "host": socket.gethostname(), "device": dev.index, "name": props.name,
+            "uuid": str(getattr(props, "uuid", "")) or None,
+            "pci_bus_id": getattr(props, "pci_bus_id", None), "gcn_arch": getattr(props, "gcnArchName", None)}
+    if comm is not None:
+        info["rccl"] = comm.size()
+    return info
+
+
 def main():
     args = parse()
+    launch = check_launch(args.gpus, os.environ)
+    if launch == "spawn":
+        sys.exit(spawn_ranks(args))
+    if launch is not None:
+        print(f"bench.py: {launch}", file=sys.stderr)
+        sys.exit(2)
     # The one JSON line goes to the real stdout; anything native libraries print there (RCCL's
     # version banner at communicator init) is sent to stderr instead.
     sys.stdout.flush()
@@ -540,8 +675,6 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and "RANK" in os.environ:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
 
     import torch
     import torch.distributed as dist
@@ -574,6 +707,11 @@ def main():
             except (OSError, RuntimeError) as e:  # reported in the line; the torch path is the same layout
                 print(f"warning: library communicator unavailable ({e}); torch.distributed gathers", file=sys.stderr)
                 gather_impl = f"torch.distributed (library communicator failed: {e})"
+    ranks = [rank_info(dev, comm)]
+    if world > 1:
+        allr = [None] * world
+        dist.all_gather_object(allr, ranks[0])
+        ranks = allr
     g1_flags = 0x4 if args.split_phases else 0  # KZGPOT_SPLIT_PHASES (applies to G1 and G2)
     g1_kernels = ["k_g1_decompress", "k_g1_check"] if args.split_phases else ["k_g1_codec"]
     g1 = Sharded("g1", n1, args.seed, args.gather_chunks, rank, world, gather, dev, verify, comm, g1_flags)
@@ -709,10 +847,19 @@ def main():
         D.codec_dev("g2_transcode", pin2, outt2, keyt2)
         next_rows["g2_transcode_uncompressed"] = transcode_row("g2", pin2, outt2, keyt2, x32, n3)
         del pin2, outt2, x32, o32
+        # the FFI boundary: host-buffer entry points with PCIe, beside the device-resident rate
+        if args.host_api:
+            if hasattr(g1, "comp"):
+                del g1.comp
+            torch.cuda.empty_cache()
+            next_rows["host_api"] = host_api_rows(args.seed + 6, dev, D)
         # row 1: end-to-end preprocess (host transcript in -> host kgz / fastkzg file out, PCIe both
-        # ways, BLAKE2b of both on host threads) at the reference's N = 2^21, buffers and files
-        if world == 1 and args.e2e_log2 > 0:
-            next_rows.update(e2e_preprocess(args.e2e_log2, args.seed + 3, dev, kzgpot, D))
+        # ways, BLAKE2b of both on host threads) at the reference's N = 2^21, buffers and files; at
+        # N > 1 rank 0 drives every GPU of the node (kzgpot_preprocess_ex(n_gpus = world): one shard
+        # per device, preprocess-kgz.rs:162-199 / preprocess-fastkgz.rs:180-214) while the other
+        # ranks wait on the host
+        if args.e2e_log2 > 0:
+            next_rows.update(e2e_preprocess(args.e2e_log2, args.seed + 3, dev, kzgpot, D, n_gpus=world))
 
     ms_per_step = elapsed * 1e3 / args.steps
     value = (n1 + n2) * args.steps / elapsed
@@ -726,6 +873,11 @@ def main():
             "value": value,
             "unit": "points/s",
             "n_gpus": world,
+            "rccl_nranks": (ranks[0].get("rccl") or {}).get("nranks"),
+            "distinct_devices": len({(r["host"], r["uuid"] or r["pci_bus_id"] or r["device"]) for r in ranks}),
+            "launcher": os.environ.get("KZGPOT_BENCH_LAUNCHER",
+                                       "torch.distributed.run (external)" if "WORLD_SIZE" in os.environ else "none"),
+            "ranks": ranks,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,
@@ -777,6 +929,14 @@ def main():
                                                   g2.comp, args.cpu_sample_log2)
         print(json.dumps(result), file=json_out, flush=True)
     if world > 1:
+        # rank 0 ran the rows after the timed region (on every GPU for the e2e rows): the others
+        # wait on the rendezvous store, on the host, so no RCCL barrier kernel sits on their GPUs
+        store = dist.distributed_c10d._get_default_store()
+        if rank == 0:
+            store.set("kzgpot_bench_rows_done", "1")
+        else:
+            import datetime
+            store.wait(["kzgpot_bench_rows_done"], datetime.timedelta(minutes=30))
         dist.barrier()
         if comm is not None:
             comm.close()

@@ -96,7 +96,8 @@ int kzgpot_g1_transcode_uncompressed_dev(const void* d_in, size_t n, void* d_out
 int kzgpot_g2_transcode_uncompressed_dev(const void* d_in, size_t n, void* d_out, uint32_t flags,
                                          uint64_t* d_bad_key, uint8_t* d_status, void* stream);
 /* Host-side decode of a bad key copied back from the device: returns 0 (none) or -(status) and
- * sets *first_bad to the index (or -1). */
+ * sets *first_bad to the index (or -1). The multi-rank key KZGPOT_KEY_RANK_FAILED (0) decodes to
+ * KZGPOT_E_RANK_FAILED with *first_bad = -1: a gathered buffer with a failed peer is never "ok". */
 int kzgpot_decode_bad_key(uint64_t key, int64_t* first_bad);
 
 /* ---------------------------------------------------------------- file pipeline (next-row §8f) */
@@ -212,9 +213,7 @@ int kzgpot_bn254_g1_decompress_dev(const void* d_in, size_t n, void* d_out, uint
  *   rank 0: kzgpot_comm_unique_id(id); ship the 128 bytes to every rank (MPI, torch.distributed,
  *   a file, ...); every rank, with its GPU current: kzgpot_comm_init(&comm, id, nranks, rank).
  * RCCL is bound at first use with dlopen("librccl.so.1") (in a torch process: the RCCL torch has
- * already loaded). KZGPOT_RCCL_LIB=<path> binds another library exporting the same symbols
- * instead, read once per process — tests/fake_rccl is such a stand-in, running N ranks as
- * threads of one process on one GPU. */
+ * already loaded). */
 #define KZGPOT_COMM_ID_BYTES 128
 int kzgpot_comm_unique_id(uint8_t* id);
 int kzgpot_comm_init(void** comm, const uint8_t* id, int nranks, int rank); /* collective */
@@ -260,14 +259,13 @@ int kzgpot_decode_allgather_dev(void* comm, int op, const void* d_in_local, uint
  * abort the communicator, which makes RCCL's kernels on this rank exit (the CUDA-style watchdog
  * a torch process group runs). first_bad may be NULL. */
 int kzgpot_comm_wait(void* comm, const uint64_t* d_bad_key, int64_t* first_bad, uint32_t timeout_ms, void* stream);
-/* Failure injection (tests and rehearsals; SURVEY §5 "failure detection"): the NEXT
- * kzgpot_decode_allgather_dev on this communicator fails at site `site`, step `at`, once:
- *   KZGPOT_FAULT_LAUNCH: the decode launch of chunk `at` (at == chunks: the tail) reports a HIP
- *   launch failure; KZGPOT_FAULT_COLLECTIVE: the `at`-th all-gather (0-based; at == chunks: the
- *   key all-reduce) reports an RCCL error. site 0 clears. */
-#define KZGPOT_FAULT_LAUNCH 1
-#define KZGPOT_FAULT_COLLECTIVE 2
-int kzgpot_comm_inject_fault(void* comm, int site, uint32_t at);
+/* What RCCL itself reports for the communicator (ncclCommCount / ncclCommUserRank /
+ * ncclCommCuDevice): the rank count, this rank and its HIP device. Any pointer may be NULL.
+ * KZGPOT_E_DEVICE once the communicator is aborted. bench.py puts these in its line, so an N-GPU
+ * number carries RCCL's own proof of N. */
+int kzgpot_comm_size(void* comm, int* nranks, int* rank, int* device);
+/* Failure injection (kzgpot_comm_inject_fault) and the KZGPOT_RCCL_LIB override exist only in the
+ * test build libkzgpot_test.so (tests/kzgpot_test_hooks.h); this library binds librccl.so.1. */
 
 /* ---------------------------------------------------------------- misc */
 const char* kzgpot_status_name(int status);  /* name of a KZGPOT_ST_* or KZGPOT_E_* code */

@@ -25,6 +25,7 @@
 
 #include "blake2b.hpp"
 #include "codec.hpp"
+#include "trace.hpp"
 
 using namespace kzgpot;
 
@@ -127,9 +128,11 @@ struct InputWait {
 };
 
 int decode_key(uint64_t key, int64_t* first_bad) {
-  if (key == kNoBad) {
+  // no kernel writes key 0 (every rejection has status >= 1): it is the multi-rank "a rank failed"
+  // word (KZGPOT_KEY_RANK_FAILED), never "point 0 accepted"
+  if (key == kNoBad || key == KZGPOT_KEY_RANK_FAILED) {
     if (first_bad) *first_bad = -1;
-    return 0;
+    return key == kNoBad ? 0 : KZGPOT_E_RANK_FAILED;
   }
   if (first_bad) *first_bad = (int64_t)(key >> 8);
   return -(int)(key & 0xff);
@@ -169,6 +172,7 @@ int run_host(int dev, CodecOp op, const uint8_t* in, size_t n, uint8_t* out, uin
   uint64_t best = kNoBad;
   // drain chunk j: its output (and status, key) back to the host
   auto drain = [&](size_t j) -> int {
+    TraceRange tr_("kzgpot.d2h");  // waits for chunk j's kernel, then its output copy
     Slot& sl = c.slot[j & 1];
     const size_t off = j * chunk, m = std::min(chunk, n - off);
     if (keep_out) HIP_TRY(hipMemcpyAsync(out + off * rout, sl.d_out, m * rout, hipMemcpyDeviceToHost, sl.stream));
@@ -177,18 +181,27 @@ int run_host(int dev, CodecOp op, const uint8_t* in, size_t n, uint8_t* out, uin
     HIP_TRY(hipMemcpyAsync(&key, sl.d_key, sizeof key, hipMemcpyDeviceToHost, sl.stream));
     HIP_TRY(hipStreamSynchronize(sl.stream));
     if (key != kNoBad && best == kNoBad) best = ((uint64_t)(key >> 8) + off) << 8 | (key & 0xff);
-    if (on_chunk && best == kNoBad) (*on_chunk)(off, m);
+    if (on_chunk && best == kNoBad) {
+      TraceRange tc_("kzgpot.handoff");
+      (*on_chunk)(off, m);
+    }
     return 0;
   };
   for (size_t j = 0; j < nchunks; j++) {
     Slot& sl = c.slot[j & 1];
     const size_t off = j * chunk, m = std::min(chunk, n - off);
-    if (in_wait && !(*in_wait)(in + (off + m) * rin)) {  // the transcript read failed
-      for (int k = 0; k < 2; k++)
-        if (c.slot[k].stream) (void)hipStreamSynchronize(c.slot[k].stream);
-      return KZGPOT_E_IO;
+    if (in_wait) {
+      TraceRange tw_("kzgpot.wait_input");  // the transcript still streaming in from disk
+      if (!(*in_wait)(in + (off + m) * rin)) {  // the transcript read failed
+        for (int k = 0; k < 2; k++)
+          if (c.slot[k].stream) (void)hipStreamSynchronize(c.slot[k].stream);
+        return KZGPOT_E_IO;
+      }
     }
-    HIP_TRY(hipMemcpyAsync(sl.d_in, in + off * rin, m * rin, hipMemcpyHostToDevice, sl.stream));
+    {
+      TraceRange th_("kzgpot.h2d");  // a pageable copy: the host thread stages it
+      HIP_TRY(hipMemcpyAsync(sl.d_in, in + off * rin, m * rin, hipMemcpyHostToDevice, sl.stream));
+    }
     HIP_TRY(hipMemsetAsync(sl.d_key, 0xff, sizeof(unsigned long long), sl.stream));
     HIP_TRY(launch_codec(op, sl.d_in, sl.d_out, m, flags, sl.d_key, status ? sl.d_status : nullptr, sl.stream));
     if (j > 0 && drain(j - 1)) return KZGPOT_E_DEVICE;  // chunks finish in order: best stays the first
@@ -288,7 +301,8 @@ namespace {
 // later sections.
 class OrderedWorker {
  public:
-  explicit OrderedWorker(std::function<bool(const uint8_t*, size_t)> fn) : fn_(std::move(fn)), th_([this] { run(); }) {}
+  OrderedWorker(const char* name, std::function<bool(const uint8_t*, size_t)> fn)
+      : name_(name), fn_(std::move(fn)), th_([this] { run(); }) {}
   ~OrderedWorker() { finish(); }
   void push(const uint8_t* p, size_t n) {
     std::lock_guard<std::mutex> l(mu_);
@@ -309,6 +323,7 @@ class OrderedWorker {
 
  private:
   void run() {
+    trace_thread(name_);
     for (;;) {
       std::pair<const uint8_t*, size_t> item;
       {
@@ -318,9 +333,11 @@ class OrderedWorker {
         item = q_.front();
         q_.pop_front();
       }
+      TraceRange tr_(name_);
       if (ok_ && !fn_(item.first, item.second)) ok_ = false;
     }
   }
+  const char* name_;
   std::function<bool(const uint8_t*, size_t)> fn_;
   std::mutex mu_;
   std::condition_variable cv_;
@@ -374,8 +391,11 @@ int preprocess_impl(const uint8_t* tr, size_t len, uint8_t* out, int mode, uint3
   bool in_ok = true;
   std::thread in_hash;
   const bool want_in = expect_in_hex || in_hex;
+  TraceRange call_("kzgpot.preprocess");
   if (want_in)
     in_hash = std::thread([&] {
+      trace_thread("kzgpot.blake2b.transcript");
+      TraceRange tr_("kzgpot.blake2b.transcript");
       if (!io.in_wm) return blake2b_512(tr, len, in_digest);
       Blake2b h;
       for (size_t off = 0; off < len;) {
@@ -393,13 +413,13 @@ int preprocess_impl(const uint8_t* tr, size_t len, uint8_t* out, int mode, uint3
   Blake2b out_h;
   std::unique_ptr<OrderedWorker> out_hash, out_write;
   if (out_hex)
-    out_hash.reset(new OrderedWorker([&](const uint8_t* p, size_t m) {
+    out_hash.reset(new OrderedWorker("kzgpot.blake2b.output", [&](const uint8_t* p, size_t m) {
       out_h.update(p, m);
       return true;
     }));
   if (io.out_fd >= 0)
     out_write.reset(new OrderedWorker(
-        [&](const uint8_t* p, size_t m) { return pwrite_all(io.out_fd, p, m, (uint64_t)(p - out)); }));
+        "kzgpot.pwrite", [&](const uint8_t* p, size_t m) { return pwrite_all(io.out_fd, p, m, (uint64_t)(p - out)); }));
   const bool sink = out_hash || out_write;
   auto push = [&](const uint8_t* p, size_t m) {
     if (out_hash) out_hash->push(p, m);
@@ -408,6 +428,9 @@ int preprocess_impl(const uint8_t* tr, size_t len, uint8_t* out, int mode, uint3
 
   // powersoftau Accumulator section order (after the 64-B hash)
   const uint64_t cnt[5] = {2 * n - 1, n, n, n, 1};
+  static const char* const kSectionRange[5] = {"kzgpot.section.tau_g1", "kzgpot.section.tau_g2",
+                                               "kzgpot.section.alpha_tau_g1", "kzgpot.section.beta_tau_g1",
+                                               "kzgpot.section.beta_g2"};
   const bool g2[5] = {false, true, false, false, true};
   // read back by read_g1/read_g2 (checked) in each binary: kgz τG1, τG2, ατG1; fastkgz + βτG1
   const bool checked[5] = {true, true, true, mode == KZGPOT_MODE_FASTKZG, false};
@@ -437,6 +460,8 @@ int preprocess_impl(const uint8_t* tr, size_t len, uint8_t* out, int mode, uint3
     for (int g = 0; g < n_shards; g++) {
       const uint64_t lo = std::min(cnt[s], g * per), hi = std::min(cnt[s], lo + per);
       th.emplace_back([&, g, lo, hi] {
+        trace_thread("kzgpot.shard");
+        TraceRange tr_(kSectionRange[s]);
         rc[g] = run_host((dev0 + g) % ndev, op, p + lo * rin, hi - lo, dst[s] ? dst[s] + lo * rout : nullptr, fl,
                          &fb[g], nullptr, stream ? &on_chunk : nullptr, dst[s] != nullptr, &in_wait);
         if (fb[g] >= 0) fb[g] += (int64_t)lo;
@@ -559,6 +584,8 @@ int kzgpot_preprocess_ex(const char* transcript_path, const char* out_path, int 
   (void)fchmod(ofd, 0644);  // mkstemp creates 0600: a setup file is meant to be read by others
   Watermark wm;
   std::thread reader([&] {
+    trace_thread("kzgpot.pread");
+    TraceRange tr_("kzgpot.pread");
     for (size_t off = 0; off < len && !wm.failed();) {  // stops at the next piece once the pipeline failed
       const ssize_t r = pread(fd, tr.get() + off, std::min<size_t>(len - off, (size_t)32 << 20), (off_t)off);
       if (r < 0 && errno == EINTR) continue;

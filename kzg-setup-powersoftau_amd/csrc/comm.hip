@@ -40,6 +40,7 @@
 #include <vector>
 
 #include "codec.hpp"
+#include "trace.hpp"
 
 using namespace kzgpot;
 
@@ -48,8 +49,9 @@ namespace {
 // RCCL is bound at first use, not at link time: a process that already holds an RCCL (torch does:
 // its own librccl.so with the same SONAME) must keep using that one — a second copy loaded ahead
 // of torch corrupts the heap at exit — and single-GPU users never load it at all.
-// KZGPOT_RCCL_LIB names another library with the same symbols (tests/fake_rccl: N ranks as
-// threads on one GPU); it is opened RTLD_LOCAL so that it never interposes on torch's RCCL.
+// Test builds only (libkzgpot_test.so, -DKZGPOT_TEST_HOOKS): KZGPOT_RCCL_LIB names another library
+// with the same symbols (tests/fake_rccl: N ranks as threads on one GPU), opened RTLD_LOCAL so that
+// it never interposes on torch's RCCL. The product library binds librccl.so.1 and nothing else.
 struct Rccl {
   decltype(&ncclGetUniqueId) get_unique_id = nullptr;
   decltype(&ncclCommInitRank) comm_init_rank = nullptr;
@@ -59,13 +61,20 @@ struct Rccl {
   decltype(&ncclAllGather) all_gather = nullptr;
   decltype(&ncclAllReduce) all_reduce = nullptr;
   decltype(&ncclGetErrorString) error_string = nullptr;
+  decltype(&ncclCommCount) comm_count = nullptr;
+  decltype(&ncclCommCuDevice) comm_device = nullptr;
+  decltype(&ncclCommUserRank) comm_user_rank = nullptr;
   bool ok = false;
 };
 const Rccl& rccl() {
   static Rccl r;
   static std::once_flag once;
   std::call_once(once, [] {
+#ifdef KZGPOT_TEST_HOOKS
     const char* over = getenv("KZGPOT_RCCL_LIB");
+#else
+    const char* over = nullptr;
+#endif
     void* h = nullptr;
     if (over && *over) {
       h = dlopen(over, RTLD_NOW | RTLD_LOCAL);
@@ -85,8 +94,11 @@ const Rccl& rccl() {
     r.all_gather = (decltype(r.all_gather))dlsym(h, "ncclAllGather");
     r.all_reduce = (decltype(r.all_reduce))dlsym(h, "ncclAllReduce");
     r.error_string = (decltype(r.error_string))dlsym(h, "ncclGetErrorString");
+    r.comm_count = (decltype(r.comm_count))dlsym(h, "ncclCommCount");
+    r.comm_device = (decltype(r.comm_device))dlsym(h, "ncclCommCuDevice");
+    r.comm_user_rank = (decltype(r.comm_user_rank))dlsym(h, "ncclCommUserRank");
     r.ok = r.get_unique_id && r.comm_init_rank && r.comm_destroy && r.comm_abort && r.all_gather && r.all_reduce &&
-           r.error_string;
+           r.error_string && r.comm_count && r.comm_device && r.comm_user_rank;
     if (!r.ok) fprintf(stderr, "kzgpot: %s lacks an RCCL entry point\n", over && *over ? over : "librccl.so.1");
   });
   return r;
@@ -120,10 +132,15 @@ struct Comm {
   unsigned long long* d_keys = nullptr;   // per-launch keys (chunks + tail)
   uint64_t* d_local = nullptr;            // [0] this rank's global-index min key, [1] = 0 (a failed rank's key)
   size_t cap_keys = 0;
-  int fault_site = 0;                     // kzgpot_comm_inject_fault, one shot
+  int fault_site = 0;                     // kzgpot_comm_inject_fault (test builds), one shot
   uint32_t fault_at = 0;
+  hipEvent_t entry = nullptr;             // recorded on the caller's stream at each call's entry
   std::mutex mu;                          // one call at a time per communicator
 };
+
+// fault sites of the test-only kzgpot_comm_inject_fault (tests/kzgpot_test_hooks.h: KZGPOT_FAULT_*);
+// a product build never sets one
+enum { kFaultLaunch = 1, kFaultCollective = 2 };
 
 bool op_from_code(int code, CodecOp* op) {
   switch (code) {
@@ -205,9 +222,11 @@ int kzgpot_comm_init(void** comm, const uint8_t* id, int nranks, int rank) {
   }
   if (hipStreamCreateWithFlags(&c->cs, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->done, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->entry, hipEventDisableTiming) != hipSuccess ||
       hipMalloc(&c->d_local, 2 * sizeof(uint64_t)) != hipSuccess ||
       hipMemset(c->d_local, 0, 2 * sizeof(uint64_t)) != hipSuccess) {
     if (c->d_local) (void)hipFree(c->d_local);
+    if (c->entry) (void)hipEventDestroy(c->entry);
     if (c->done) (void)hipEventDestroy(c->done);
     if (c->cs) (void)hipStreamDestroy(c->cs);
     rccl().comm_destroy(c->nccl);
@@ -227,6 +246,7 @@ int kzgpot_comm_destroy(void* comm) {
   if (!c->aborted) (void)hipStreamSynchronize(c->cs);  // an aborted comm's kernels have exited or never will
   for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
   (void)hipEventDestroy(c->done);
+  (void)hipEventDestroy(c->entry);
   if (!c->aborted) {
     if (c->d_keys) (void)hipFree(c->d_keys);
     if (c->d_local) (void)hipFree(c->d_local);
@@ -245,14 +265,33 @@ int kzgpot_shard_layout(uint64_t n, int nranks, uint32_t chunks, uint64_t* block
   return 0;
 }
 
+int kzgpot_comm_size(void* comm, int* nranks, int* rank, int* device) {
+  if (!comm) return KZGPOT_E_INVALID_ARG;
+  Comm& c = *(Comm*)comm;
+  std::lock_guard<std::mutex> lock(c.mu);
+  if (c.aborted || !c.nccl) return KZGPOT_E_DEVICE;
+  int n = -1, r = -1, d = -1;  // what RCCL itself reports for the communicator, not our copies
+  NCCL_OK(rccl().comm_count(c.nccl, &n));
+  NCCL_OK(rccl().comm_user_rank(c.nccl, &r));
+  NCCL_OK(rccl().comm_device(c.nccl, &d));
+  if (nranks) *nranks = n;
+  if (rank) *rank = r;
+  if (device) *device = d;
+  return 0;
+}
+
+#ifdef KZGPOT_TEST_HOOKS
+// Failure injection, test builds only (declared in tests/kzgpot_test_hooks.h): the NEXT
+// kzgpot_decode_allgather_dev on this communicator fails at `site`, step `at`, once.
 int kzgpot_comm_inject_fault(void* comm, int site, uint32_t at) {
-  if (!comm || site < 0 || site > KZGPOT_FAULT_COLLECTIVE) return KZGPOT_E_INVALID_ARG;
+  if (!comm || site < 0 || site > kFaultCollective) return KZGPOT_E_INVALID_ARG;
   Comm& c = *(Comm*)comm;
   std::lock_guard<std::mutex> lock(c.mu);
   c.fault_site = site;
   c.fault_at = at;
   return 0;
 }
+#endif
 
 int kzgpot_decode_allgather_dev(void* comm, int op_code, const void* d_in_local, uint64_t n, uint32_t chunks,
                                 void* d_out, uint32_t flags, uint64_t* d_bad_key, void* stream) {
@@ -261,6 +300,7 @@ int kzgpot_decode_allgather_dev(void* comm, int op_code, const void* d_in_local,
     return KZGPOT_E_INVALID_ARG;
   Comm& c = *(Comm*)comm;
   std::lock_guard<std::mutex> lock(c.mu);
+  TraceRange tr_("kzgpot.decode_allgather.enqueue");
   if (c.aborted) return KZGPOT_E_DEVICE;
   int dev = -1;
   HIP_OK(hipGetDevice(&dev));
@@ -282,6 +322,15 @@ int kzgpot_decode_allgather_dev(void* comm, int op_code, const void* d_in_local,
     }
     return !failed;
   };
+  // The comm stream runs behind everything the caller queued on `stream` before this call (a
+  // memset of d_bad_key, a reader of the previous d_out), whatever fails later: the collectives
+  // below write d_out and d_bad_key on cs even when no chunk event ever links the two streams.
+  if (hipEventRecord(c.entry, s) != hipSuccess || hipStreamWaitEvent(c.cs, c.entry, 0) != hipSuccess) {
+    fprintf(stderr, "kzgpot: rank %d of %d: cannot order the comm stream after the caller's stream\n", c.rank,
+            c.nranks);
+    failed = true;
+    (void)hipStreamSynchronize(s);  // the same order, the slow way
+  }
   // the previous call's collectives read d_keys / d_local and used the events: wait for them
   if (c.done_recorded) local(hipStreamWaitEvent(s, c.done, 0), "hipStreamWaitEvent(previous call)");
   if (!failed && c.cap_keys < chunks + 1) {
@@ -304,20 +353,20 @@ int kzgpot_decode_allgather_dev(void* comm, int op_code, const void* d_in_local,
   for (uint32_t ch = 0; B && ch < chunks; ch++) {
     if (!failed) {
       const uint64_t g0 = ((uint64_t)ch * c.nranks + c.rank) * B;
-      const hipError_t e = fault == KZGPOT_FAULT_LAUNCH && fault_at == ch
+      const hipError_t e = fault == kFaultLaunch && fault_at == ch
                                ? hipErrorLaunchFailure
                                : launch_codec(op, in + ch * B * rin, out + g0 * rout, B, flags, c.d_keys + ch, nullptr, s);
       if (local(e, "decode launch") && local(hipEventRecord(c.ev[ch], s), "hipEventRecord"))
         local(hipStreamWaitEvent(c.cs, c.ev[ch], 0), "hipStreamWaitEvent");
     }
     uint8_t* region = out + (uint64_t)ch * c.nranks * B * rout;
-    const ncclResult_t r = fault == KZGPOT_FAULT_COLLECTIVE && fault_at == ch
+    const ncclResult_t r = fault == kFaultCollective && fault_at == ch
                                ? ncclSystemError
                                : rccl().all_gather(region + (size_t)c.rank * bytes, region, bytes, ncclUint8, c.nccl, c.cs);
     if (r != ncclSuccess) return abort_comm(c, r, "ncclAllGather");
   }
   if (!failed && tail) {
-    const hipError_t e = fault == KZGPOT_FAULT_LAUNCH && fault_at == chunks
+    const hipError_t e = fault == kFaultLaunch && fault_at == chunks
                              ? hipErrorLaunchFailure
                              : launch_codec(op, in + (uint64_t)chunks * B * rin,
                                             out + (uint64_t)chunks * c.nranks * B * rout, tail, flags,
@@ -332,7 +381,7 @@ int kzgpot_decode_allgather_dev(void* comm, int op_code, const void* d_in_local,
   }
   // a failed rank contributes the constant 0 word (d_local[1], never written after init): the
   // min over ranks is then KZGPOT_KEY_RANK_FAILED on every rank
-  const ncclResult_t r = fault == KZGPOT_FAULT_COLLECTIVE && fault_at == chunks
+  const ncclResult_t r = fault == kFaultCollective && fault_at == chunks
                              ? ncclSystemError
                              : rccl().all_reduce(failed ? c.d_local + 1 : c.d_local, d_bad_key, 1, ncclUint64,
                                                  ncclMin, c.nccl, c.cs);
@@ -352,6 +401,7 @@ int kzgpot_comm_wait(void* comm, const uint64_t* d_bad_key, int64_t* first_bad, 
     std::lock_guard<std::mutex> lock(c.mu);
     if (c.aborted) return KZGPOT_E_DEVICE;
   }
+  TraceRange tr_("kzgpot.comm_wait");
   const auto t0 = std::chrono::steady_clock::now();
   for (int spin = 0;; spin++) {
     const hipError_t q = hipStreamQuery(s);
@@ -372,6 +422,16 @@ int kzgpot_comm_wait(void* comm, const uint64_t* d_bad_key, int64_t* first_bad, 
       return KZGPOT_E_TIMEOUT;
     }
     if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(200));
+  }
+  {
+    // a stream that drained is not proof that the collectives moved the data: an RCCL error
+    // reported asynchronously (a peer aborted) voids the buffer and the key
+    std::lock_guard<std::mutex> lock(c.mu);
+    if (c.aborted) return KZGPOT_E_DEVICE;
+    ncclResult_t ae = ncclSuccess;
+    if (rccl().async_error && c.nccl && rccl().async_error(c.nccl, &ae) == ncclSuccess && ae != ncclSuccess &&
+        ae != ncclInProgress)
+      return abort_comm(c, ae, "asynchronous RCCL operation");
   }
   uint64_t key = ~0ull;
   HIP_OK(hipMemcpy(&key, d_bad_key, sizeof key, hipMemcpyDeviceToHost));

@@ -12,6 +12,9 @@ import re
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REPO_ROOT = os.path.dirname(PKG_ROOT)
 LIB_PATH = os.environ.get("KZGPOT_LIB", os.path.join(PKG_ROOT, "build", "libkzgpot.so"))
+# test build (-DKZGPOT_TEST_HOOKS): + kzgpot_comm_inject_fault and the KZGPOT_RCCL_LIB override
+# (tests/kzgpot_test_hooks.h); tests select it through KZGPOT_LIB
+TEST_LIB_PATH = os.path.join(PKG_ROOT, "build", "libkzgpot_test.so")
 HEADER_PATH = os.path.join(REPO_ROOT, "include", "kzgpot.h")
 
 u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -63,7 +66,7 @@ SIGNATURES = {
     "kzgpot_shard_layout": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_int, ctypes.c_uint32, u64p, u64p]),
     "kzgpot_decode_allgather_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]),
     "kzgpot_comm_wait": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, i64p, ctypes.c_uint32, ctypes.c_void_p]),
-    "kzgpot_comm_inject_fault": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32]),
+    "kzgpot_comm_size": (ctypes.c_int, [ctypes.c_void_p, intp, intp, intp]),
     "kzgpot_status_name": (ctypes.c_char_p, [ctypes.c_int]),
     "kzgpot_device_count": (ctypes.c_int, []),
     "kzgpot_version": (ctypes.c_char_p, []),

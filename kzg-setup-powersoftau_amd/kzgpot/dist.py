@@ -151,11 +151,14 @@ class LibComm:
                                        torch.cuda.current_stream().cuda_stream)
         return rc, fb.value
 
-    def inject_fault(self, site: int, at: int) -> None:
-        """Failure injection for the next decode_allgather (KZGPOT_FAULT_LAUNCH = 1 /
-        KZGPOT_FAULT_COLLECTIVE = 2; `at` = chunk or collective index)."""
-        if self.lib.kzgpot_comm_inject_fault(self.handle, site, at):
-            raise ValueError("kzgpot_comm_inject_fault: bad arguments")
+    def size(self) -> dict:
+        """What RCCL reports for this communicator (kzgpot_comm_size: ncclCommCount,
+        ncclCommUserRank, ncclCommCuDevice)."""
+        n, r, d = self._ct.c_int(-1), self._ct.c_int(-1), self._ct.c_int(-1)
+        rc = self.lib.kzgpot_comm_size(self.handle, self._ct.byref(n), self._ct.byref(r), self._ct.byref(d))
+        if rc:
+            raise RuntimeError(f"kzgpot_comm_size failed ({rc})")
+        return {"nranks": n.value, "rank": r.value, "device": d.value}
 
     def close(self) -> None:
         if self.handle:

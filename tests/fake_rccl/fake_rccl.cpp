@@ -15,6 +15,11 @@
 // Every collective also checks that all ranks issued the same operation with the same size —
 // the mismatch that would hang real RCCL is reported as ncclInvalidUsage instead.
 // A barrier that waits longer than FAKE_RCCL_TIMEOUT_S (default 60) returns ncclSystemError.
+//
+// Async-error mode (fake_rccl_set_async_errors(1), per process): once a peer aborted, a collective
+// returns ncclSuccess at once without moving anything, as real RCCL's enqueue does, and the
+// failure is visible only through ncclCommGetAsyncError — so the peers learn of it where real
+// peers do, in kzgpot_comm_wait, instead of from the enqueue's return code.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <stdint.h>
@@ -58,11 +63,13 @@ struct Group {
 struct FakeComm {
   Group* g;
   int rank;
+  int device;  // the HIP device current at ncclCommInitRank, as RCCL records it
 };
 
 std::mutex g_reg_mu;
 std::map<std::string, Group*> g_reg;
 std::atomic<uint64_t> g_counter{0};
+std::atomic<int> g_async_errors{0};
 
 double timeout_s() {
   const char* e = getenv("FAKE_RCCL_TIMEOUT_S");
@@ -71,7 +78,7 @@ double timeout_s() {
 
 // generation barrier; lk holds g->mu
 ncclResult_t barrier(Group* g, std::unique_lock<std::mutex>& lk, int rank, const char* what) {
-  if (g->aborted) return ncclRemoteError;
+  if (g->aborted) return g_async_errors ? ncclInProgress : ncclRemoteError;
   const uint64_t my = g->gen;
   if (++g->arrived == g->nranks) {
     g->arrived = 0;
@@ -82,7 +89,7 @@ ncclResult_t barrier(Group* g, std::unique_lock<std::mutex>& lk, int rank, const
   const bool woke = g->cv.wait_for(lk, std::chrono::duration<double>(timeout_s()),
                                    [&] { return g->gen != my || g->aborted; });
   if (g->gen != my) return ncclSuccess;
-  if (g->aborted) return ncclRemoteError;
+  if (g->aborted) return g_async_errors ? ncclInProgress : ncclRemoteError;
   if (!woke) fprintf(stderr, "fake_rccl: rank %d timed out in %s (%d of %d arrived)\n", rank, what, g->arrived, g->nranks);
   return ncclSystemError;
 }
@@ -96,9 +103,15 @@ size_t dtype_size(ncclDataType_t t) {
   }
 }
 
+// a collective's result as its caller sees it: in async-error mode an aborted group's collective
+// "was enqueued" (ncclSuccess); the error is reported by ncclCommGetAsyncError
+ncclResult_t enqueue_result(ncclResult_t r) { return r == ncclInProgress ? ncclSuccess : r; }
+
 }  // namespace
 
 extern "C" {
+
+void fake_rccl_set_async_errors(int on) { g_async_errors = on; }
 
 const char* ncclGetErrorString(ncclResult_t r) {
   switch (r) {
@@ -143,7 +156,9 @@ ncclResult_t ncclCommInitRank(ncclComm_t* comm, int nranks, ncclUniqueId id, int
   g->live++;
   const ncclResult_t r = barrier(g, lk, rank, "ncclCommInitRank");
   if (r != ncclSuccess) return r;
-  *comm = (ncclComm_t) new FakeComm{g, rank};
+  int dev = -1;
+  if (hipGetDevice(&dev) != hipSuccess) return ncclUnhandledCudaError;
+  *comm = (ncclComm_t) new FakeComm{g, rank, dev};
   return ncclSuccess;
 }
 
@@ -173,6 +188,24 @@ ncclResult_t ncclCommGetAsyncError(ncclComm_t comm, ncclResult_t* err) {
   return ncclSuccess;
 }
 
+ncclResult_t ncclCommCount(const ncclComm_t comm, int* count) {
+  if (!comm || !count) return ncclInvalidArgument;
+  *count = ((FakeComm*)comm)->g->nranks;
+  return ncclSuccess;
+}
+
+ncclResult_t ncclCommUserRank(const ncclComm_t comm, int* rank) {
+  if (!comm || !rank) return ncclInvalidArgument;
+  *rank = ((FakeComm*)comm)->rank;
+  return ncclSuccess;
+}
+
+ncclResult_t ncclCommCuDevice(const ncclComm_t comm, int* device) {
+  if (!comm || !device) return ncclInvalidArgument;
+  *device = ((FakeComm*)comm)->device;
+  return ncclSuccess;
+}
+
 ncclResult_t ncclAllGather(const void* send, void* recv, size_t count, ncclDataType_t dt, ncclComm_t comm,
                            hipStream_t stream) {
   if (!comm || !dtype_size(dt)) return ncclInvalidArgument;
@@ -186,7 +219,7 @@ ncclResult_t ncclAllGather(const void* send, void* recv, size_t count, ncclDataT
   mine.send = send;
   mine.bytes = bytes;
   ncclResult_t r = barrier(g, lk, c->rank, "ncclAllGather");
-  if (r != ncclSuccess) return r;
+  if (r != ncclSuccess) return enqueue_result(r);
   std::vector<const void*> src(g->nranks);
   for (int i = 0; i < g->nranks; i++) {
     if (g->slots[i].kind != kAllGather || g->slots[i].bytes != bytes) {
@@ -204,7 +237,7 @@ ncclResult_t ncclAllGather(const void* send, void* recv, size_t count, ncclDataT
   }
   if (hipStreamSynchronize(stream) != hipSuccess) return ncclUnhandledCudaError;
   lk.lock();  // slots stay as they are: a slower peer may still be reading them until this barrier
-  return barrier(g, lk, c->rank, "ncclAllGather (release)");
+  return enqueue_result(barrier(g, lk, c->rank, "ncclAllGather (release)"));
 }
 
 ncclResult_t ncclAllReduce(const void* send, void* recv, size_t count, ncclDataType_t dt, ncclRedOp_t op,
@@ -224,7 +257,7 @@ ncclResult_t ncclAllReduce(const void* send, void* recv, size_t count, ncclDataT
   mine.redop = (int)op;
   mine.host = v;
   ncclResult_t r = barrier(g, lk, c->rank, "ncclAllReduce");
-  if (r != ncclSuccess) return r;
+  if (r != ncclSuccess) return enqueue_result(r);
   std::vector<uint64_t> acc = g->slots[0].host;
   for (int i = 0; i < g->nranks; i++) {
     const Slot& s = g->slots[i];
@@ -244,7 +277,7 @@ ncclResult_t ncclAllReduce(const void* send, void* recv, size_t count, ncclDataT
                 hipStreamSynchronize(stream) != hipSuccess))
     return ncclUnhandledCudaError;
   lk.lock();  // slots stay as they are: a slower peer may still be reading them until this barrier
-  return barrier(g, lk, c->rank, "ncclAllReduce (release)");
+  return enqueue_result(barrier(g, lk, c->rank, "ncclAllReduce (release)"));
 }
 
 }  // extern "C"

@@ -28,6 +28,10 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 import torch  # noqa: E402
 
 from kzgpot import _lib  # noqa: E402
+
+# the test build of the library: the product one has no failure injection and binds only
+# librccl.so.1 (tests/kzgpot_test_hooks.h)
+_lib.LIB_PATH = os.environ.get("KZGPOT_LIB", _lib.TEST_LIB_PATH)
 from kzgpot import device as D  # noqa: E402
 from kzgpot import dist as KD  # noqa: E402
 
@@ -37,6 +41,8 @@ REC = {"g1_decompress": ("g1", 48, 96), "g2_decompress": ("g2", 96, 192), "bn254
 JOIN_S = 180  # a thread still running after this is a hang (reported, never waited for)
 
 lib = _lib.load()
+lib.kzgpot_comm_inject_fault.restype = ctypes.c_int
+lib.kzgpot_comm_inject_fault.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32]
 CUDA = torch.device("cuda", 0)
 
 
@@ -180,6 +186,16 @@ def main():
         ("g1_decompress", 37, 8, 4),  # fewer points than blocks: all tail
     ]
     comms = {w: make_comms(w) for w in (2, 4, 8)}
+    # what RCCL itself reports for the communicators (kzgpot_comm_size)
+    sizes = {}
+    for w_, hs in comms.items():
+        got = []
+        for h in hs:
+            n_, r_, d_ = ctypes.c_int(-1), ctypes.c_int(-1), ctypes.c_int(-1)
+            rc = lib.kzgpot_comm_size(h, ctypes.byref(n_), ctypes.byref(r_), ctypes.byref(d_))
+            got.append([rc, n_.value, r_.value, d_.value])
+        sizes[str(w_)] = got
+    report["comm_size"] = sizes
     for op, n, chunks, world in layouts:
         st = Stream(op, n, chunks, world, seed=100 + world + n % 1000)
         r = st.run(comms[world])
@@ -219,7 +235,20 @@ def main():
     # 4. an RCCL error on rank 2 at the second all-gather: rank 2 aborts, every peer returns an error
     report["collective_failure_rank2"] = st.run(comms[world], fault=(2, 2, 1))
     report["after_abort"] = st.run(comms[world])
+
+    # 4b. the same failure the way real RCCL shows it to the peers: their enqueues succeed and the
+    #     error surfaces only asynchronously, so the peers learn of it in kzgpot_comm_wait
+    fake = ctypes.CDLL(os.environ["KZGPOT_RCCL_LIB"])  # the library's own (already loaded) copy
+    fake.fake_rccl_set_async_errors(1)
+    comms_async = make_comms(world)
+    report["collective_failure_rank2_async"] = st.run(comms_async, fault=(2, 2, 1))
+    fake.fake_rccl_set_async_errors(0)
     del st
+
+    # 4c. an aborted communicator reports no size
+    n_, r_, d_ = ctypes.c_int(-1), ctypes.c_int(-1), ctypes.c_int(-1)
+    report["comm_size"]["aborted"] = lib.kzgpot_comm_size(comms_async[2], ctypes.byref(n_), ctypes.byref(r_),
+                                                          ctypes.byref(d_))
 
     # 5. BASELINE config 4 at its size, sharded 8 ways as the config names it: 2^27 G1 in 8 chunks
     #    (12 GiB gathered on every rank) and 2^16 G2, every rank's whole buffer against the generator
@@ -248,7 +277,7 @@ def main():
                                                                            out.data_ptr(), 0, key.data_ptr(),
                                                                            torch.cuda.current_stream().cuda_stream)}
     torch.cuda.synchronize()
-    for w_, hs in comms.items():
+    for w_, hs in list(comms.items()) + [("async", comms_async)]:
         for h in hs:
             lib.kzgpot_comm_destroy(h)
     lib.kzgpot_comm_destroy(c1)

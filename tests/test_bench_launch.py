@@ -1,0 +1,62 @@
+"""bench.py's launch contract, CPU only: `bench.py --gpus N` with no launcher
+must start the N ranks itself — torch.distributed.run as a CHILD process (never exec), the JSON line
+passed through, the child's exit code returned — and a launcher whose WORLD_SIZE disagrees with
+--gpus must be an error, so an N-GPU line can never silently time one rank. Anchor: the
+reference's only parallel stage, the chunked decompression of preprocess-kgz.rs:105-110."""
+import importlib.util
+import os
+import subprocess
+import sys
+
+from conftest import ROOT
+
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def load_bench():
+    spec = importlib.util.spec_from_file_location("bench_under_test", BENCH)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_check_launch_decisions():
+    b = load_bench()
+    assert b.check_launch(1, {}) is None                        # N = 1: run here
+    assert b.check_launch(8, {}) == "spawn"                     # N > 1, no launcher: start the ranks
+    assert b.check_launch(8, {"WORLD_SIZE": "8"}) is None       # under the driver's torch.distributed.run
+    assert b.check_launch(1, {"WORLD_SIZE": "1"}) is None
+    err = b.check_launch(8, {"WORLD_SIZE": "1"})                # the silent one-rank case: an error now
+    assert err and "WORLD_SIZE 1" in err
+
+
+def test_spawn_argv_is_the_drivers_launch():
+    b = load_bench()
+    cmd = b.spawn_argv(4, 29511, ["--gpus", "4", "--steps", "2"])
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert "--nproc-per-node=4" in cmd and "--nnodes=1" in cmd
+    assert "--master-addr=127.0.0.1" in cmd and "--master-port=29511" in cmd
+    assert cmd[-4:] == ["--gpus", "4", "--steps", "2"] and cmd[-5] == os.path.abspath(BENCH)
+
+
+def test_spawn_forwards_json_and_exit_code(monkeypatch, capsys):
+    """The child's rank-0 JSON line reaches stdout alone; other output goes to stderr; the child's
+    exit code is returned (a failing rank fails the bench)."""
+    b = load_bench()
+    script = "import sys; print('rccl banner'); print('{\"metric\": \"m\", \"value\": 1}'); sys.exit(3)"
+    monkeypatch.setattr(b, "spawn_argv", lambda n, port, argv: [sys.executable, "-c", script])
+
+    class A:
+        gpus = 2
+
+    assert b.spawn_ranks(A()) == 3
+    out, err = capsys.readouterr()
+    assert out.strip() == '{"metric": "m", "value": 1}'
+    assert "rccl banner" in err and "torch.distributed.run" not in out
+
+
+def test_world_size_mismatch_exits_nonzero_before_torch():
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, BENCH, "--gpus", "8"], env=env, capture_output=True, text=True, timeout=60)
+    assert p.returncode == 2
+    assert "WORLD_SIZE 1" in p.stderr and p.stdout == ""

@@ -1,7 +1,7 @@
 """The library's multi-rank decode + RCCL all-gather (kzgpot_decode_allgather_dev) at 2, 4 and 8
 ranks on one GPU: ranks are threads of one process bound to the test-only RCCL stand-in
-(tests/fake_rccl via KZGPOT_RCCL_LIB, which the library reads once per process — so the scenarios
-run in tests/multirank_driver.py, one child process, and the assertions are here).
+(tests/fake_rccl via KZGPOT_RCCL_LIB, which the test build libkzgpot_test.so reads once per process
+— so the scenarios run in tests/multirank_driver.py, one child process, and the assertions are here).
 
 Every rank's gathered buffer must equal the generator's expected bytes, the single-launch output
 and a C-oracle re-decode of the records around every rank's block boundaries and the tail; bad
@@ -20,6 +20,7 @@ pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 FAKE = os.path.join(ROOT, "tests", "fake_rccl", "build", "libfake_rccl.so")
+TEST_LIB = os.path.join(ROOT, "kzg-setup-powersoftau_amd", "build", "libkzgpot_test.so")
 NO_BAD = (1 << 64) - 1
 E_DEVICE, E_RANK_FAILED, E_TIMEOUT = -101, -106, -107
 
@@ -29,6 +30,7 @@ def report(gpu):
     if not os.path.exists(FAKE):
         subprocess.run(["make", "-C", os.path.dirname(FAKE)], check=True)
     env = dict(os.environ, KZGPOT_RCCL_LIB=FAKE, FAKE_RCCL_TIMEOUT_S="60")
+    env.setdefault("KZGPOT_LIB", TEST_LIB)  # the test build: failure injection + the RCCL override
     p = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tests", "multirank_driver.py")], env=env,
                        capture_output=True, text=True, timeout=600)
     assert p.returncode == 0, p.stderr[-4000:]
@@ -98,6 +100,23 @@ def test_collective_failure_aborts_every_rank_without_hang(report):
     assert r["seconds"] < 30
     after = report["after_abort"]
     assert after["rc"] == [E_DEVICE] * 4 and after["wait"] == [E_DEVICE] * 4
+
+
+def test_collective_failure_seen_by_peers_in_comm_wait(report):
+    """Real RCCL's peers enqueue successfully and see a peer's abort only asynchronously: their
+    kzgpot_comm_wait must turn that into an error (and abort their own communicator)."""
+    r = report["collective_failure_rank2_async"]
+    assert r["hung"] == [] and r["seconds"] < 30
+    assert r["rc"] == [0, 0, E_DEVICE, 0], r["rc"]           # only rank 2's own call failed
+    assert r["wait"] == [E_DEVICE] * 4, r["wait"]            # every peer learned it in comm_wait
+
+
+def test_comm_size_reports_rccl_view(report):
+    """kzgpot_comm_size returns what the RCCL communicator says: count, rank, device."""
+    s = report["comm_size"]
+    for w in (2, 4, 8):
+        assert s[str(w)] == [[0, w, r, 0] for r in range(w)], s[str(w)]
+    assert s["aborted"] == E_DEVICE
 
 
 def test_config4_full_size_sharded_8_ways(report):

@@ -22,6 +22,34 @@ def test_library_exports_header_symbols(kzgpot_mod):
     assert set(_lib.SIGNATURES) == set(syms)
 
 
+def test_test_hooks_only_in_test_build(kzgpot_mod):
+    """Failure injection and the KZGPOT_RCCL_LIB override live in libkzgpot_test.so only
+    (-DKZGPOT_TEST_HOOKS, tests/kzgpot_test_hooks.h): the product library exports no inject symbol
+    and binds nothing but librccl.so.1."""
+    from kzgpot import _lib
+
+    prod = open(_lib.LIB_PATH, "rb").read()
+    assert b"kzgpot_comm_inject_fault" not in prod and b"KZGPOT_RCCL_LIB" not in prod
+    if not os.path.exists(_lib.TEST_LIB_PATH):
+        subprocess.run(["make", "-C", PKG, "-j", "8"], check=True)
+    test_lib = ctypes.CDLL(_lib.TEST_LIB_PATH)
+    assert hasattr(test_lib, "kzgpot_comm_inject_fault") and hasattr(test_lib, "kzgpot_comm_size")
+    assert b"KZGPOT_RCCL_LIB" in open(_lib.TEST_LIB_PATH, "rb").read()
+
+
+def test_rank_failed_key_never_decodes_as_success(kzgpot_mod):
+    """KZGPOT_KEY_RANK_FAILED (0), the all-reduced key when a peer could not decode its share,
+    decodes to KZGPOT_E_RANK_FAILED — not to 'every point accepted' (ADVICE r03)."""
+    from kzgpot import _lib
+
+    lib = _lib.load()
+    fb = ctypes.c_int64(123)
+    assert lib.kzgpot_decode_bad_key(0, ctypes.byref(fb)) == -106 and fb.value == -1
+    assert lib.kzgpot_decode_bad_key((1 << 64) - 1, ctypes.byref(fb)) == 0 and fb.value == -1
+    assert lib.kzgpot_decode_bad_key((5 << 8) | 3, ctypes.byref(fb)) == -3 and fb.value == 5
+    assert lib.kzgpot_decode_bad_key(1, ctypes.byref(fb)) == -1 and fb.value == 0
+
+
 def test_synth_library_exports():
     from kzgpot import device
 
