@@ -159,7 +159,12 @@ int run_host(int dev, CodecOp op, const uint8_t* in, size_t n, uint8_t* out, uin
   DeviceGuard guard;
   HIP_TRY(hipSetDevice(dev));
   const uint64_t rin = in_record(op), rout = out_record(op);
-  const size_t chunk = std::min<size_t>(n, (size_t)1 << 21);  // 2 x 2^21 x 288 B of staging at most
+  // 2 x 2^21 x 288 B of staging at most. A call of up to 2^24 points is cut into at least 8 chunks
+  // (multiples of the 256-point block, at least 2^17 points = one full wave of blocks on 256 CUs)
+  // so that its PCIe copies overlap its kernels: only the first H2D and the last D2H stay exposed
+  // (2^20 G2 points in one chunk: 31 % over the device-resident time, profiles/r04a_bench_n1.json)
+  size_t chunk = std::min<size_t>(n, (size_t)1 << 21);
+  if (n > ((size_t)2 << 17)) chunk = std::min(chunk, std::max<size_t>((size_t)1 << 17, ((n + 7) / 8 + 255) & ~(size_t)255));
   const size_t nchunks = (n + chunk - 1) / chunk;
   for (int k = 0; k < (nchunks > 1 ? 2 : 1); k++) {
     Slot& sl = c.slot[k];

@@ -24,6 +24,7 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "kzg-setup-powersoftau_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 import torch  # noqa: E402
 
@@ -93,7 +94,7 @@ class Stream:
         kind, self.rin, self.rout = REC[op]
         self.op, self.n, self.chunks, self.world = op, n, chunks, world
         comp, self.exp = D.synth(kind, seed, 0, n, CUDA)
-        self.comp = comp.clone()
+        self.comp = comp.clone() if damage else comp
         for i in damage:
             self.comp[i * self.rin] &= 0x7F  # compression bit cleared: UnexpectedCompressionMode (status 1)
         self.local = []
@@ -147,6 +148,30 @@ def single_rank_output(st):
     D.codec_dev(st.op, st.comp, out, key)
     torch.cuda.synchronize()
     return out, D.read_key(key)
+
+
+def bn254_oracle_sample(st, out, per_edge=8):
+    """Config 5 has no C restatement: the Python oracle (oracle/kzgpot_oracle.py, ark-bn254 0.2
+    deserialize + serialize_uncompressed) re-decodes `per_edge` records at both edges of every
+    rank's block in the first and last chunk, compared with one rank's gathered buffer."""
+    import kzgpot_oracle as O
+
+    b, tail = KD.shard_layout(st.n, st.world, st.chunks)
+    starts = set()
+    for c in (0, st.chunks - 1):
+        for r in range(st.world):
+            g0 = (c * st.world + r) * b
+            starts.update((g0, max(0, g0 + b - per_edge)))
+    ok, pts = True, 0
+    for s0 in sorted(starts):
+        m = min(per_edge, st.n - s0)
+        data = bytes(st.comp[s0 * st.rin:(s0 + m) * st.rin].cpu().numpy())
+        got = bytes(out[s0 * st.rout:(s0 + m) * st.rout].cpu().numpy())
+        for i in range(m):
+            status, want = O.bn254_g1_decompress_point(data[i * 32:(i + 1) * 32])
+            ok = ok and status == 0 and got[i * 64:(i + 1) * 64] == want
+        pts += m
+    return {"points": pts, "equal": bool(ok), "oracle": "oracle/kzgpot_oracle.py bn254_g1_decompress_point"}
 
 
 def oracle_sample(st, out, oracle):
@@ -261,6 +286,20 @@ def main():
         report[f"config4_full/{op}/world=8"] = r
         del st
         torch.cuda.empty_cache()
+
+    # 5b. BASELINE config 5 at its size, sharded 8 ways as the config names it: 2^28 BN254 G1 in 8
+    #     chunks, 16 GiB gathered on every rank (8 x 16 GiB of outputs on the one GPU), every rank's
+    #     whole buffer against the generator, and a Python-oracle sample around the rank boundaries
+    t5 = time.time()
+    st = Stream("bn254_g1_decompress", 1 << 28, 8, 8, seed=45)
+    r = st.run(comms[8], timeout_ms=300_000)
+    r["equal_expected"] = st.equal_expected()
+    r["layout"] = dict(zip(("block", "tail"), KD.shard_layout(1 << 28, 8, 8)))
+    r["oracle"] = bn254_oracle_sample(st, st.outs[5])
+    r["case_seconds"] = time.time() - t5
+    report["config5_full/bn254_g1_decompress/world=8"] = r
+    del st
+    torch.cuda.empty_cache()
 
     # 6. the host watchdog: kzgpot_comm_wait on a stream still busy after timeout_ms aborts the comm
     (c1,) = make_comms(1)

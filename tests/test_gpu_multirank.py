@@ -44,7 +44,7 @@ def report(gpu):
 
 
 def test_every_rank_holds_the_whole_stream(report):
-    cases = [k for k in report if "/world=" in k and not k.startswith("config4_full")]
+    cases = [k for k in report if "/world=" in k and not k.startswith(("config4_full", "config5_full"))]
     assert len(cases) == 8
     for k in cases:
         r = report[k]
@@ -127,6 +127,18 @@ def test_config4_full_size_sharded_8_ways(report):
         assert r["hung"] == [] and r["rc"] == [0] * 8 and r["wait"] == [0] * 8, (op, r["rc"], r["wait"])
         assert r["equal_expected"] == [True] * 8, op
     assert report["config4_full/g1_decompress/world=8"]["layout"] == {"block": 1 << 21, "tail": 0}
+
+
+def test_config5_full_size_sharded_8_ways(report):
+    """BASELINE config 5 (BN254 2^28 G1 on 8 GPUs) through the library call at 8 ranks: every
+    rank ends with the whole 16 GiB arkworks buffer, bit-exact against the generator, and the
+    records at both edges of every rank's block in the first and last chunk equal the Python
+    oracle's decode (ark-bn254 deserialize + serialize_uncompressed)."""
+    r = report["config5_full/bn254_g1_decompress/world=8"]
+    assert r["hung"] == [] and r["rc"] == [0] * 8 and r["wait"] == [0] * 8, (r["rc"], r["wait"])
+    assert r["equal_expected"] == [True] * 8
+    assert r["layout"] == {"block": 1 << 22, "tail": 0}
+    assert r["oracle"]["equal"] and r["oracle"]["points"] == 2 * 8 * 2 * 8
 
 
 def test_wait_watchdog_times_out_and_aborts(report):
