@@ -65,57 +65,6 @@ KZG_DEV void jac_dbl(jac<fp>& p) {
   fp_negk_nr<BlsFp::KB_2_28>(p.y, d);     // Y3                    < 2^29
 }
 
-// 3P from the affine base (x, y) (Z = 1): EFD tpl-2007-bl with Z1 = 1 —
-//   XX = x^2, YY = y^2, YYYY = YY^2, M = 3 XX, E = 6 ((x + YY)^2 - XX - YYYY) - M^2, T = 16 YYYY,
-//   U = (M + E)^2 - M^2 - E^2 - T, X3 = 4 (x E^2 - 4 YY U), Y3 = 8 y (U (T - U) - E E^2), Z3 = 2E.
-// 7S + two two-product reductions + 1M, where the fast ladders' first two steps (|u| starts with the
-// bits 11: a doubling from Z = 1, then a mixed addition) took 3S + 2M + a multiply-plus-square and
-// 3S + 6M + a two-product reduction. Only the endomorphism tests use it (points ON the curve, where
-// any formula for 3P gives the same point); the reference-algorithm ladder keeps ark's operations.
-// In: x any ladder value (the second G1 ladder's base Q1.X is lazy), y limbs < 2^30. Out: X3 limbs
-// < 2^30, Y3 and Z3 normalized. Bounds: tests/field_bounds_model.py jac_tpl_affine_fp.
-KZG_DEV void jac_tpl_affine(jac<fp>& p) {
-  fp x, xx, yy, yyyy, m, mm, s, e, ee, t, u, n, w;
-  fp_norm(x, p.x);                              // x                      N
-  fp_sqr(xx, x);                                // XX                     N
-  fp_sqr(yy, p.y);                              // YY                     N
-  fp_sqr(yyyy, yy);                             // YYYY                   N
-  fp_mul3_nr(m, xx);
-  fp_norm(m, m);                                // M = 3 XX               N
-  fp_sqr(mm, m);                                // MM                     N
-  fp_add_nr(s, x, yy);
-  fp_sqr(s, s);                                 // S1 = (x + YY)^2        N
-  fp_subk_nr<BlsFp::KB_8_28>(s, s, xx);
-  fp_subk_nr<BlsFp::KB_8_28>(s, s, yyyy);
-  fp_norm(w, s);                                // w = S1 - XX - YYYY = 2 x YY   N
-  fp_shl_nr<1>(s, w);
-  fp_mul3_nr(s, s);                             // 6w
-  fp_subk_nr<BlsFp::KB_8_28>(s, s, mm);
-  fp_norm(e, s);                                // E = 6w - MM            N
-  fp_sqr(ee, e);                                // EE                     N
-  fp_shl_nr<3>(t, yyyy);
-  fp_norm(t, t);
-  fp_shl_nr<1>(t, t);                           // T = 16 YYYY           < 2^29
-  fp_add_nr(s, m, e);
-  fp_sqr(s, s);                                 // S2 = (M + E)^2         N
-  fp_subk_nr<BlsFp::KB_8_28>(s, s, mm);
-  fp_subk_nr<BlsFp::KB_16_28>(s, s, ee);
-  fp_subk_nr<BlsFp::KB_32_29>(s, s, t);
-  fp_norm(u, s);                                // U = S2 - MM - EE - T   N
-  fp_negk_nr<BlsFp::KB_128_28>(n, u);           // -U                    < 2^29
-  fp_shl_nr<2>(w, yy);                          // 4 YY                  < 2^30
-  fp_mul_sum2(s, x, ee, w, n);                  // x EE - 4 YY U          N
-  fp_shl_nr<2>(p.x, s);                         // X3                    < 2^30
-  fp_subk_nr<BlsFp::KB_128_28>(w, t, u);        // T - U                 < 2^30
-  fp_negk_nr<BlsFp::KB_16_28>(n, ee);           // -EE                   < 2^29
-  fp_mul_sum2(s, u, w, e, n);                   // U (T - U) - E EE       N
-  fp_mul(s, p.y, s);
-  fp_shl_nr<3>(s, s);
-  fp_norm(p.y, s);                              // Y3 = 8 y (...)         N
-  fp_shl_nr<1>(s, e);
-  fp_norm(p.z, s);                              // Z3 = 2E                N
-}
-
 // ---------------------------------------------------------------- G1 fast ladders, W = 2Y
 // The endomorphism test's ladders (in_subgroup_fast_g1) carry W = 2Y instead of Y: then
 // B' = W^2 = 4B, D = X B' and Z3 = W Z need no 4X / 2Y, and -W3 = 2E (X3 - D) + B'^2 needs no
@@ -309,57 +258,6 @@ KZG_DEV void jac_dbl(jac<fp2>& p) {
   fp_shl_nr<1>(s, b.c0);                     // 2 b0                < 2^29
   fp_mul_sum3(p.y.c1, a.c0, d.c1, a.c1, d.c0, s, n);
   p.y.c0 = c0;                               // Y3 = E (D - X3) - 8 B^2
-}
-
-// G2 tripling from the affine base, as the G1 one (EFD tpl-2007-bl with Z1 = 1) but returned as
-// the equivalent triple (X3/4, Y3/8, Z3/2) = (x EE - 4 YY U, y (U (T - U) - E EE), E), which drops
-// the final x4 / x8 / x2 and their normalizations, and with E = 12 x YY - MM from a product
-// instead of (x + YY)^2 - XX - YYYY: a multiply for a squaring, but E's value stays ~14 p, small
-// enough to serve as Z (the doubling's and the mixed addition's borrowed constants for Z are
-// KB_16_28). The base is fetched twice (load), so that x and y are not held across the formula:
-// at most five Fp2 values live. Out: normalized. Bounds: tests/field_bounds_model.py
-// jac_tpl_affine_fp2_lz (joined into ladder_invariant_fp2_lz).
-template <typename Load>
-KZG_DEV void jac_tpl_affine(jac<fp2>& p, Load&& load) {
-  fp2 yy, m, s, ee, t;
-  load(p.x, p.y);
-  f2_sqr_lz<BlsFp::KB_2_28>(m, p.x);         // XX
-  f2_sqr_lz<BlsFp::KB_2_28>(yy, p.y);        // YY
-  f2_mul_lz<BlsFp::KB_2_28>(p.z, p.x, yy);   // x YY                (x, y dead)
-  fp_mul3_nr(m.c0, m.c0);
-  fp_mul3_nr(m.c1, m.c1);
-  f2_norm(m, m);                             // M = 3 XX
-  f2_sqr_lz<BlsFp::KB_4_28>(t, m);           // MM
-  fp_mul3_nr(p.z.c0, p.z.c0);
-  fp_mul3_nr(p.z.c1, p.z.c1);
-  f2_shl<2>(p.z, p.z);
-  f2_subk<BlsFp::KB_2_28>(p.z, p.z, t);
-  f2_norm(p.z, p.z);                         // E = 12 x YY - MM = Z3
-  f2_add_nr(s, m, p.z);
-  f2_norm(s, s);
-  f2_sqr_lz<BlsFp::KB_32_28>(s, s);          // S2 = (M + E)^2
-  f2_subk<BlsFp::KB_2_28>(s, s, t);          // - MM
-  f2_sqr_lz<BlsFp::KB_16_28>(ee, p.z);       // EE
-  f2_subk<BlsFp::KB_4_28>(s, s, ee);         // - EE
-  f2_sqr_lz<BlsFp::KB_2_28>(t, yy);          // YYYY
-  f2_shl<3>(t, t);
-  f2_norm(t, t);
-  f2_shl<1>(t, t);                           // T = 16 YYYY
-  f2_subk<BlsFp::KB_32_29>(s, s, t);
-  f2_norm(s, s);                             // U = S2 - MM - EE - T
-  f2_subk<BlsFp::KB_64_28>(t, t, s);
-  f2_norm(t, t);                             // T - U
-  f2_mul_lz<BlsFp::KB_128_28>(t, s, t);      // U (T - U)
-  f2_shl<2>(yy, yy);
-  f2_mul_lz<BlsFp::KB_64_28>(yy, yy, s);     // 4 YY U
-  f2_mul_lz<BlsFp::KB_2_28>(m, p.z, ee);     // E EE
-  f2_subk<BlsFp::KB_2_28>(t, t, m);
-  f2_norm(t, t);                             // U (T - U) - E EE
-  load(p.x, p.y);
-  f2_mul_lz<BlsFp::KB_2_28>(p.x, p.x, ee);   // x EE
-  f2_subk<BlsFp::KB_2_28>(p.x, p.x, yy);
-  f2_norm(p.x, p.x);                         // X3 / 4 = x EE - 4 YY U
-  f2_mul_lz<BlsFp::KB_8_28>(p.y, p.y, t);    // Y3 / 8 = y (U (T - U) - E EE)
 }
 
 // G2 mixed addition (ark add_assign_mixed incl. its zero / equal-point branches, as jac_madd):
@@ -589,7 +487,7 @@ KZG_DEV void jac_madd(jac<F>& p, Load&& load) {
 }
 
 // [|u|] B for the affine finite base B delivered by load(x, y): |u| starts with the bits 11, so
-// the first doubling and mixed addition are one tripling from the affine base (jac_tpl_affine);
+// the first doubling and mixed addition are one tripling from the affine base (jac_tpl_affine_w);
 // then 61 doublings, 4 mixed additions.
 template <typename F, typename Load>
 KZG_DEV void mul_abs_u_affine(jac<F>& acc, Load&& load) {

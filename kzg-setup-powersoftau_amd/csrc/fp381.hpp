@@ -511,7 +511,8 @@ struct f30 {
 };
 KZG_DEV int32_t sext30(uint32_t x) { return __builtin_amdgcn_sbfe((int32_t)x, 0, 30); }
 
-// r = a b 2^-390 mod p for balanced a, b (|digit| <= 2^29, top digit < 2^22); r balanced with
+// r = a b 2^-390 mod p for balanced a, b (|digit| <= 2^29, |top digit| <= 2^23: the bound
+// tests/test_fp30.py proves, TOP_IN = 2^23 + 1, and the exponentiation's callers use); r balanced with
 // |value| < p/2 + |a| |b| / R30. The lower columns are made divisible by 2^30 by m_i = balanced
 // (col * PINV30); the upper columns start their a*b partial sum at +2^29, so that the digit
 // (acc & M30) - 2^29 and the carry acc >> 30 are the balanced remainder and its exact quotient.
@@ -585,7 +586,8 @@ KZG_DEV void f30_sqr(f30& r, const f30& a) {
   }
   r.v[N - 1] = (int32_t)acc;
 }
-// the same integer in balanced 30-bit digits; a: limbs < 2^32 - 16, value < 2^380
+// the same integer in balanced 30-bit digits; a: limbs < 2^32 - 16, value < 2^383 (proven in
+// tests/test_fp30.py and test_field_bounds._pow_pm3d4: fp2_sqrt's norm input reaches ~2.02 p)
 KZG_DEV void f30_from_fp(f30& r, const fp& a) {
   fp n;
   fp_norm(n, a);

@@ -361,33 +361,6 @@ def jac_dbl_fp(X, Y, Z):
     return x3, y3, z3
 
 
-def jac_tpl_affine_fp(x, y):
-    """jac_tpl_affine(jac<fp>&) — 3P from the affine base (x, y): tpl-2007-bl with Z1 = 1 (Z3 = 2E),
-    7S + 2 two-product reductions + 1M, the lazy forms of curve.hpp."""
-    x = norm(x, "x")  # the second G1 ladder's base Q1.X is a lazy ladder value
-    xx = sqr(x, "XX")
-    yy = sqr(y, "YY")
-    yyyy = sqr(yy, "YYYY")
-    m = norm(mul3(xx), "M")
-    mm = sqr(m, "MM")
-    s1 = sqr(add_nr(x, yy), "S1")
-    w = norm(subk(subk(s1, xx, "KB_8_28", "S1-XX"), yyyy, "KB_8_28", "S1-XX-YYYY"), "2 x YY")
-    e = norm(subk(mul3(shl(w, 1)), mm, "KB_8_28", "6w-MM"), "E")
-    ee = sqr(e, "EE")
-    t = shl(norm(shl(yyyy, 3), "8 YYYY"), 1)  # T = 16 YYYY   < 2^29
-    s2 = sqr(add_nr(m, e), "S2")
-    u = subk(subk(subk(s2, mm, "KB_8_28", "S2-MM"), ee, "KB_16_28", "-EE"), t, "KB_32_29", "-T")
-    u = norm(u, "U")
-    nu = subk(normalized(0), u, "KB_128_28", "-U")
-    x3 = shl(mul_sum2(x, ee, shl(yy, 2), nu, "x EE - 4 YY U"), 2)
-    tu = subk(t, u, "KB_128_28", "T-U")
-    nee = subk(normalized(0), ee, "KB_16_28", "-EE")
-    inner = mul_sum2(u, tu, e, nee, "U (T - U) - E EE")
-    y3 = norm(shl(mul(y, inner, "y inner"), 3), "Y3")
-    z3 = norm(shl(e, 1), "Z3=2E")
-    return x3, y3, z3
-
-
 # ---- the G1 fast ladders in W = 2Y coordinates (curve.hpp jac_dbl_w / jac_madd_w / jac_tpl_affine_w)
 def jac_dbl_w(X, W, Z):
     """jac_dbl_w: A = X^2, B' = W^2, D = X B', E = 3A, Z3 = W Z, X3 = F - 2D,
@@ -543,9 +516,8 @@ def _within(F, a, b):
 def ladder_invariant(F, base_x, base_y, rounds=12):
     """A bound set S for the ladder accumulator (X, Y, Z) that contains the starting point and is
     CLOSED under one ladder step (dbl, then optionally madd(base)) — hence bounds every state
-    reached by mul_abs_u_affine / in_subgroup_ref for any input. Found by joined iteration, then
-    inflated and verified closed. For G1 the set also contains the fast ladder's first step, the
-    tripling of the affine base (jac_tpl_affine: |u| starts with bits 11)."""
+    reached by in_subgroup_ref (ark's double-and-add) for any input. Found by joined iteration, then
+    inflated and verified closed. (The fast ladders run in W = 2Y coordinates: ladder_invariant_w.)"""
     X, Y, Z = base_x, base_y, F.one()
 
     def step(X, Y, Z):
@@ -555,10 +527,6 @@ def ladder_invariant(F, base_x, base_y, rounds=12):
         for ox, oy, oz in outs:
             nx, ny, nz = join(F, nx, ox), join(F, ny, oy), join(F, nz, oz)
         return nx, ny, nz
-
-    if not F.two:
-        tx, ty, tz = jac_tpl_affine_fp(base_x, base_y)
-        X, Y, Z = join(F, X, tx), join(F, Y, ty), join(F, Z, tz)
 
     for _ in range(rounds):
         X, Y, Z = step(X, Y, Z)
@@ -634,33 +602,6 @@ def add2(a, b, name="add2"):
     return V2(add_nr(a.c0, b.c0, name), add_nr(a.c1, b.c1, name))
 
 
-def jac_tpl_affine_fp2_lz(x, y):
-    """curve.hpp jac_tpl_affine(jac<fp2>&): 3P from the normalized affine base (x, y), returned as
-    the equivalent Jacobian triple (X3/4, Y3/8, Z3/2) = (x EE - 4 YY U, y (U (T - U) - E EE), E),
-    with E = 12 x YY - MM from a product (value ~14 p: Z must stay below 16 p for the doubling's
-    borrowed constant); outputs normalized (the G2 ladder discipline)."""
-    xx = sqr2(x, "KB_2_28", "XX")
-    yy = sqr2(y, "KB_2_28", "YY")
-    yyyy = sqr2(yy, "KB_2_28", "YYYY")
-    m = norm2(mul3_2(xx), "M")
-    mm = sqr2(m, "KB_4_28", "MM")
-    w = mul2(x, yy, "KB_2_28", "x YY")
-    e = norm2(subk2(shl2(mul3_2(w), 2), mm, "KB_2_28", "12 x YY - MM"), "E")
-    ee = sqr2(e, "KB_16_28", "EE")
-    t = shl2(norm2(shl2(yyyy, 3), "8YYYY"), 1)
-    s2 = sqr2(norm2(add2(m, e), "M+E"), "KB_32_28", "S2")
-    u = subk2(subk2(subk2(s2, mm, "KB_2_28", "S2-MM"), ee, "KB_4_28", "-EE"), t, "KB_32_29", "-T")
-    u = norm2(u, "U")
-    a = mul2(x, ee, "KB_2_28", "xEE")
-    b = mul2(shl2(yy, 2), u, "KB_64_28", "4YYU")
-    x3 = norm2(subk2(a, b, "KB_2_28", "xEE-4YYU"), "X3/4")
-    c = mul2(u, norm2(subk2(t, u, "KB_64_28", "T-U"), "T-U"), "KB_128_28", "U(T-U)")
-    d = mul2(e, ee, "KB_2_28", "E EE")
-    inner = norm2(subk2(c, d, "KB_2_28", "inner"), "inner")
-    y3 = mul2(y, inner, "KB_8_28", "Y3/8")
-    return x3, y3, e
-
-
 def jac_madd_fp2_lz(X, Y, Z, x2, y2):
     """curve.hpp jac_madd(jac<fp2>&, load): normalized in / out; base (x2, y2) normalized."""
     z1z1 = sqr2(Z, "KB_16_28", "Z1Z1")
@@ -720,8 +661,6 @@ def ladder_invariant_fp2_lz(base_x, base_y, rounds=12):
         return nx, ny, nz
 
     X, Y, Z = base_x, base_y, V2(normalized(1), normalized(0))
-    tx, ty, tz = jac_tpl_affine_fp2_lz(base_x, base_y)  # the fast ladder's first step: 3 B
-    X, Y, Z = join2(X, tx), join2(Y, ty), join2(Z, tz)
     for _ in range(rounds):
         X, Y, Z = step(X, Y, Z)
     S = (infl(X), infl(Y), infl(Z))

@@ -7,8 +7,9 @@ on subgroup points, on random curve points outside the subgroup and on small-ord
   jac_dbl (G1)            -Y3 = E (X3 - D) + 8 B^2   (fp_mul_add8sqr)
   jac_dbl (G2)            Y3 = E (D - X3) - 8 B^2 as two three-product sums per component
   jac_madd                ark add_assign_mixed with r' = S2 - Y1 (r = 2 r') and Z3 = 2 Z1 H
-  jac_tpl_affine (G1)     EFD tpl-2007-bl with Z1 = 1: (X3, Y3, 2E)
-  jac_tpl_affine (G2)     the equivalent triple (X3 / 4, Y3 / 8, E), E = 12 x YY - MM
+  tpl_g1 / tpl_g2         the Y-form tripling (EFD tpl-2007-bl with Z1 = 1; G2 as the triple
+                          (X3 / 4, Y3 / 8, E), E = 12 x YY - MM): reference-only, the algebra the
+                          device's W = 2Y forms jac_tpl_affine_w (tpl_g1_w / tpl_g2_w) scale
   mul_abs_u_affine        [|u|] B: the tripling, then 61 doublings and 4 mixed additions
   in_subgroup_fast_g1     [u^2] P as [|u|] of Q1 = (X : Y : Z) run on y^2 = x^3 + 4 Z^6 from the
                           affine (X, Y), mapped back by Z' -> Z' Z; compared with phi(P) = (beta x, -y)

@@ -14,13 +14,24 @@ sys.path.insert(0, os.path.join(ROOT, "kzg-setup-powersoftau_amd"))
 
 
 def main():
+    import argparse
+
     import torch
     from kzgpot import _lib
     from kzgpot import device as D
     from kzgpot import dist as KD
 
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--log2s", default="20", help="comma-separated sizes (a per-launch constant vs a per-point cost)")
+    a = ap.parse_args()
     dev = torch.device("cuda", 0)
-    n = 1 << 20
+    res = {}
+    for lg in (int(x) for x in a.log2s.split(",")):
+        res[lg] = run_size(1 << lg, dev, torch, D, KD)
+    print(json.dumps({"bit_exact": res, "lib": _lib.LIB_PATH}))
+
+
+def run_size(n, dev, torch, D, KD):
     ok = {}
     c1, x1 = D.synth("g1", 11, 0, n, dev)
     c2, x2 = D.synth("g2", 12, 0, n, dev)
@@ -38,7 +49,7 @@ def main():
         torch.cuda.synchronize()
         ok[name] = bool(D.read_key(key) == KD.NO_BAD and torch.equal(out, want))
         del out
-    print(json.dumps({"points": n, "bit_exact": ok, "lib": _lib.LIB_PATH}))
+    return ok
 
 
 if __name__ == "__main__":

@@ -28,8 +28,12 @@ def read(path):
                     d = per[key][int(r.get("Dispatch_Id") or r.get("Correlation_Id"))]
                     d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
                     d["_grid"] = int(r["Grid_Size"])
-    # the last dispatch of each kernel (fetch_probe.py launches each twice)
-    return {k: v[max(v)] for k, v in per.items()}
+    # per (kernel, grid size): the last dispatch (fetch_probe.py launches each twice per size)
+    out = {}
+    for k, v in per.items():
+        for did in sorted(v):
+            out[(k, v[did]["_grid"])] = v[did]
+    return out
 
 
 def main():
@@ -41,18 +45,27 @@ def main():
         f = read(glob.glob(os.path.join(d, "FETCH_SIZE", "**", "*counter_collection.csv"), recursive=True)[0])
         w = read(glob.glob(os.path.join(d, "WRITE_SIZE", "**", "*counter_collection.csv"), recursive=True)[0])
         ic = read(glob.glob(os.path.join(d, "SQC_ICACHE_MISSES", "**", "*counter_collection.csv"), recursive=True)[0])
+        rq_files = glob.glob(os.path.join(d, "TCC_EA0_RDREQ_sum", "**", "*counter_collection.csv"), recursive=True)
+        rq = read(rq_files[0]) if rq_files else {}
         rows = {}
-        for k in NAMES.values():
-            if k not in f:
-                continue
-            n = f[k]["_grid"]
-            rd = 2 * 1024 * f[k]["FETCH_SIZE"] / n
-            wr = 1024 * w[k]["WRITE_SIZE"] / n if k in w else None
-            miss = ic.get(k, {}).get("SQC_ICACHE_MISSES")
-            rows[k] = {"points": n, "fetch_B_per_point": round(rd, 2), "write_B_per_point": None if wr is None else round(wr, 2),
-                       "algorithmic_read_write": ALG[k], "fetch_excess_B_per_point": round(rd - ALG[k][0], 2),
-                       "icache_misses_per_point": None if miss is None else round(miss / n, 3),
-                       "valu_per_wave": None if k not in ic else round(ic[k].get("SQ_INSTS_VALU", 0) / max(1, ic[k].get("SQ_WAVES", 1)))}
+        for (k, n) in sorted(f):
+            rd = 2 * 1024 * f[(k, n)]["FETCH_SIZE"] / n
+            wr = 1024 * w[(k, n)]["WRITE_SIZE"] / n if (k, n) in w else None
+            c = ic.get((k, n), {})
+            r = rq.get((k, n), {})
+            row = {"points": n, "fetch_B_per_point": round(rd, 3), "write_B_per_point": None if wr is None else round(wr, 3),
+                   "algorithmic_read_write": ALG[k], "fetch_excess_B_per_point": round(rd - ALG[k][0], 3),
+                   "fetch_excess_MB_per_launch": round((rd - ALG[k][0]) * n / 1e6, 3),
+                   "icache_misses_per_point": round(c["SQC_ICACHE_MISSES"] / n, 3) if "SQC_ICACHE_MISSES" in c else None,
+                   "valu_per_wave": round(c.get("SQ_INSTS_VALU", 0) / max(1, c.get("SQ_WAVES", 1))) if c else None}
+            if r:
+                tot = r.get("TCC_EA0_RDREQ_sum", 0)
+                b32, b128 = r.get("TCC_EA0_RDREQ_32B_sum", 0), r.get("TCC_EA0_RDREQ_128B_sum", 0)
+                row["rdreq"] = {"total": tot, "32B": b32, "128B": b128, "64B": tot - b32 - b128,
+                                "dram": r.get("TCC_EA0_RDREQ_DRAM_sum"),
+                                "bytes_by_size_per_point": round((32 * b32 + 128 * b128 + 64 * (tot - b32 - b128)) / n, 3),
+                                "sqc_inst_req": r.get("SQC_TC_INST_REQ"), "sqc_data_read_req": r.get("SQC_TC_DATA_READ_REQ")}
+            rows[f"{k} @ {n}"] = row
         out["builds"][lib] = rows
     print(json.dumps(out, indent=1))
 
