@@ -614,10 +614,25 @@ def spawn_ranks(args) -> int:
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:  # a free rendezvous port
         sk.bind(("127.0.0.1", 0))
         port = sk.getsockname()[1]
+    import signal
+
     cmd = spawn_argv(args.gpus, port, sys.argv[1:])
     env = dict(os.environ, KZGPOT_BENCH_LAUNCHER="bench.py -> torch.distributed.run (child process)")
     print(f"bench.py: --gpus {args.gpus}: starting {' '.join(cmd)}", file=sys.stderr, flush=True)
-    p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True)
+
+    def die_with_parent():  # the launcher (and through it every rank) gets SIGTERM if this process dies
+        try:
+            ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, signal.SIGTERM)  # PR_SET_PDEATHSIG
+        except OSError:
+            pass
+
+    p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True, preexec_fn=die_with_parent)
+
+    def forward(sig, _frame):  # a timeout's SIGTERM / a ^C reaches the launcher, which stops its ranks
+        p.send_signal(sig)
+
+    for sig in (signal.SIGTERM, signal.SIGINT):
+        signal.signal(sig, forward)
     for line in p.stdout:
         if line.startswith("{") and '"metric"' in line:
             sys.stdout.write(line)

@@ -55,6 +55,40 @@ def test_spawn_forwards_json_and_exit_code(monkeypatch, capsys):
     assert "rccl banner" in err and "torch.distributed.run" not in out
 
 
+def test_spawned_launcher_dies_with_the_bench(tmp_path):
+    """A driver timeout kills bench.py: the launcher it started must not outlive it (it would keep
+    the ranks on the GPUs). The child is started with PR_SET_PDEATHSIG = SIGTERM."""
+    import signal
+    import time
+
+    pidfile = tmp_path / "child.pid"
+    stub = ("import os, sys, time; open(sys.argv[1], 'w').write(str(os.getpid())); time.sleep(120)")
+    driver = (
+        "import importlib.util, sys\n"
+        f"spec = importlib.util.spec_from_file_location('b', {BENCH!r}); b = importlib.util.module_from_spec(spec)\n"
+        "spec.loader.exec_module(b)\n"
+        f"b.spawn_argv = lambda n, port, argv: [sys.executable, '-c', {stub!r}, {str(pidfile)!r}]\n"
+        "class A: gpus = 2\n"
+        "sys.exit(b.spawn_ranks(A()))\n")
+    parent = subprocess.Popen([sys.executable, "-c", driver])
+    for _ in range(200):
+        if pidfile.exists() and pidfile.read_text():
+            break
+        time.sleep(0.05)
+    child = int(pidfile.read_text())
+    parent.send_signal(signal.SIGKILL)  # no chance to forward anything: only the death signal helps
+    parent.wait()
+    for _ in range(100):
+        try:
+            os.kill(child, 0)
+        except ProcessLookupError:
+            break
+        time.sleep(0.05)
+    else:
+        os.kill(child, signal.SIGKILL)
+        raise AssertionError("the spawned launcher outlived bench.py")
+
+
 def test_world_size_mismatch_exits_nonzero_before_torch():
     env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
     p = subprocess.run([sys.executable, BENCH, "--gpus", "8"], env=env, capture_output=True, text=True, timeout=60)
