@@ -94,6 +94,21 @@ def cpu_cores():
     return min(os.cpu_count() or 1, 16)  # the GPU box grants 16 CPUs per GPU
 
 
+def host_cpu():
+    """The box's CPU as SURVEY §8d asks it recorded beside the baseline: model, nproc, affinity."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), None)
+    except OSError:
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = None
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": affinity}
+
+
 def cpu_baseline(comp1, comp2, sample_log2):
     """Reference-schedule CPU timing of the oracle restatement on a bounded sample."""
     lib = oracle_lib()
@@ -117,7 +132,7 @@ def cpu_baseline(comp1, comp2, sample_log2):
     a2 = lib.oracle_g2_decompress(h2, ctypes.c_size_t(s2), o2, 0, ctypes.byref(fb), None, cores, cores)
     dt_all = time.perf_counter() - t
     return {
-        "value": (s1 + s2) / dt, "unit": "points/s", "cores": cores, "kind": "port",
+        "value": (s1 + s2) / dt, "unit": "points/s", "cores": cores, "kind": "port", **host_cpu(),
         "sample": f"{s1} G1 + {s2} G2 from the bench transcript, reference schedule "
                   f"(decompress on {cores} threads, arkworks subgroup check + serialize on 1 thread); "
                   f"{dt:.1f} s; rc={r1},{r2}",
@@ -946,13 +961,14 @@ def main():
     if world > 1:
         # rank 0 ran the rows after the timed region (on every GPU for the e2e rows): the others
         # wait on the rendezvous store, on the host, so no RCCL barrier kernel sits on their GPUs
-        store = dist.distributed_c10d._get_default_store()
-        if rank == 0:
+        get_store = getattr(dist.distributed_c10d, "_get_default_store", None)
+        store = get_store() if get_store else None
+        if store is not None and rank == 0:
             store.set("kzgpot_bench_rows_done", "1")
-        else:
+        elif store is not None:
             import datetime
             store.wait(["kzgpot_bench_rows_done"], datetime.timedelta(minutes=30))
-        dist.barrier()
+        dist.barrier()  # (without a store, this barrier alone waits for rank 0's rows)
         if comm is not None:
             comm.close()
         dist.destroy_process_group()

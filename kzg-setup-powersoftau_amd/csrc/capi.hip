@@ -9,6 +9,7 @@
 #include <errno.h>
 #include <fcntl.h>
 #include <stdlib.h>
+#include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -553,6 +554,43 @@ int kzgpot_preprocess_buffer(const uint8_t* tr, size_t len, uint8_t* out, int mo
   return preprocess_impl(tr, len, out, mode, n_log2, n_gpus, nullptr, nullptr, nullptr, bad_section, bad_index);
 }
 
+}  // extern "C"
+
+namespace {
+// A large host buffer of the file path (the 604 MB transcript, the 0.6-1.0 GB output): a 2 MiB
+// aligned anonymous mapping with MADV_HUGEPAGE, so faulting it in (pread, the D2H copies) and
+// unmapping it at the end costs one fault / one free per 2 MiB instead of per 4 KiB page (with
+// transparent huge pages in "madvise" mode; elsewhere it is an ordinary mapping).
+class HostBuf {
+ public:
+  explicit HostBuf(size_t n) {
+    constexpr size_t kHuge = (size_t)2 << 20;
+    map_ = n + kHuge;
+    void* m = mmap(nullptr, map_, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (m == MAP_FAILED) {
+      map_ = 0;
+      return;
+    }
+    base_ = (uint8_t*)m;
+    p_ = (uint8_t*)(((uintptr_t)m + kHuge - 1) & ~(uintptr_t)(kHuge - 1));
+    (void)madvise(p_, n, MADV_HUGEPAGE);
+  }
+  ~HostBuf() {
+    if (map_) munmap(base_, map_);
+  }
+  HostBuf(const HostBuf&) = delete;
+  HostBuf& operator=(const HostBuf&) = delete;
+  uint8_t* get() const { return p_; }
+
+ private:
+  size_t map_ = 0;
+  uint8_t* base_ = nullptr;
+  uint8_t* p_ = nullptr;
+};
+}  // namespace
+
+extern "C" {
+
 // File to file, as the reference runs (preprocess-kgz.rs:69-126,187-194): a reader thread streams
 // the transcript in 32 MiB pread()s while the GPU decodes what has arrived; a writer thread
 // pwrite()s each output range as it lands. The output goes to a temporary file in the same
@@ -564,6 +602,7 @@ int kzgpot_preprocess_ex(const char* transcript_path, const char* out_path, int 
   if (bad_section) *bad_section = -1;
   if (bad_index) *bad_index = -1;
   if (!transcript_path || !out_path || n_log2 < 1 || n_log2 > 30) return KZGPOT_E_INVALID_ARG;
+  TraceRange call_("kzgpot.preprocess_file");
   const int fd = open(transcript_path, O_RDONLY | O_CLOEXEC);
   if (fd < 0) return KZGPOT_E_IO;
   const off_t flen = lseek(fd, 0, SEEK_END);
@@ -573,43 +612,56 @@ int kzgpot_preprocess_ex(const char* transcript_path, const char* out_path, int 
   }
   const size_t len = (size_t)flen;
   (void)posix_fadvise(fd, 0, flen, POSIX_FADV_SEQUENTIAL);
-  std::unique_ptr<uint8_t[]> tr(new (std::nothrow) uint8_t[len]);
-  std::unique_ptr<uint8_t[]> out(new (std::nothrow) uint8_t[kzgpot_output_size(n_log2, mode)]);
-  if (!tr || !out) {
-    close(fd);
-    return KZGPOT_E_INVALID_ARG;
-  }
-  // unique per call (mkstemp), so concurrent calls for one out_path never share a temporary
+  int r = 0;
   std::string tmp = std::string(out_path) + ".kzgpot-tmp-XXXXXX";
-  const int ofd = mkostemp(&tmp[0], O_CLOEXEC);
-  if (ofd < 0) {
-    close(fd);
-    return KZGPOT_E_IO;
-  }
-  (void)fchmod(ofd, 0644);  // mkstemp creates 0600: a setup file is meant to be read by others
-  Watermark wm;
-  std::thread reader([&] {
-    trace_thread("kzgpot.pread");
-    TraceRange tr_("kzgpot.pread");
-    for (size_t off = 0; off < len && !wm.failed();) {  // stops at the next piece once the pipeline failed
-      const ssize_t r = pread(fd, tr.get() + off, std::min<size_t>(len - off, (size_t)32 << 20), (off_t)off);
-      if (r < 0 && errno == EINTR) continue;
-      if (r <= 0) return wm.fail();
-      off += (size_t)r;
-      wm.advance(off);
+  {
+    std::unique_ptr<HostBuf> tr(new HostBuf(len)), out(new HostBuf(kzgpot_output_size(n_log2, mode)));
+    if (!tr->get() || !out->get()) {
+      close(fd);
+      return KZGPOT_E_INVALID_ARG;
     }
-  });
-  PipelineIo io;
-  io.in_wm = &wm;
-  io.out_fd = ofd;
-  int r = preprocess_impl(tr.get(), len, out.get(), mode, n_log2, n_gpus, expect_transcript_digest,
-                          transcript_digest, output_digest, bad_section, bad_index, io);
-  if (r) wm.fail();  // the reader finishes its current pread and stops; nothing waits on it
-  reader.join();
-  close(fd);
-  if (close(ofd) != 0 && !r) r = KZGPOT_E_IO;
-  if (!r && rename(tmp.c_str(), out_path) != 0) r = KZGPOT_E_IO;
-  if (r) unlink(tmp.c_str());
+    // unique per call (mkstemp), so concurrent calls for one out_path never share a temporary
+    const int ofd = mkostemp(&tmp[0], O_CLOEXEC);
+    if (ofd < 0) {
+      close(fd);
+      return KZGPOT_E_IO;
+    }
+    (void)fchmod(ofd, 0644);  // mkstemp creates 0600: a setup file is meant to be read by others
+    Watermark wm;
+    std::thread reader([&] {
+      trace_thread("kzgpot.pread");
+      TraceRange tr_("kzgpot.pread");
+      for (size_t off = 0; off < len && !wm.failed();) {  // stops at the next piece once the pipeline failed
+        const ssize_t k = pread(fd, tr->get() + off, std::min<size_t>(len - off, (size_t)32 << 20), (off_t)off);
+        if (k < 0 && errno == EINTR) continue;
+        if (k <= 0) return wm.fail();
+        off += (size_t)k;
+        wm.advance(off);
+      }
+    });
+    PipelineIo io;
+    io.in_wm = &wm;
+    io.out_fd = ofd;
+    r = preprocess_impl(tr->get(), len, out->get(), mode, n_log2, n_gpus, expect_transcript_digest,
+                        transcript_digest, output_digest, bad_section, bad_index, io);
+    if (r) wm.fail();  // the reader finishes its current pread and stops; nothing waits on it
+    reader.join();
+    {
+      TraceRange fin_("kzgpot.file_finish");  // closes and rename
+      close(fd);
+      if (close(ofd) != 0 && !r) r = KZGPOT_E_IO;
+      if (!r && rename(tmp.c_str(), out_path) != 0) r = KZGPOT_E_IO;
+      if (r) unlink(tmp.c_str());
+    }
+    // Unmapping 1.2-1.6 GB of faulted-in pages takes ~77 ms of kernel time (profiles/r04e_e2e_stages.json,
+    // after_pipeline_ms) that the caller does not need to wait for: a detached thread releases them.
+    std::thread([t = std::move(tr), o = std::move(out)]() mutable {
+      trace_thread("kzgpot.release");
+      TraceRange rel_("kzgpot.file_release");
+      t.reset();
+      o.reset();
+    }).detach();
+  }
   return r;
 }
 int kzgpot_preprocess(const char* transcript_path, const char* out_path, int mode, uint32_t n_log2, int n_gpus,

@@ -101,9 +101,9 @@ def test_no_subgroup_check_mode(gpu, oracle_lib):
 
 
 def test_chunked_host_path_first_bad(gpu, oracle_lib):
-    """> 2^22 points run the host API's two-stream chunk pipeline (2^21-point chunks, three of
-    them, so a slot is reused); bad points in the second and third chunks: the smallest global
-    index is reported, every status lands at its global index."""
+    """> 2^22 points run the host API's two-stream chunk pipeline (8 chunks of 524,800 points, so
+    both slots are reused); bad points in the fourth and the last chunk: the smallest global index
+    is reported, every status lands at its global index."""
     base, ark = _random_stream(oracle_lib, 4096, seed=3)
     n = (1 << 22) + 4096
     reps = n // 4096
@@ -116,6 +116,27 @@ def test_chunked_host_path_first_bad(gpu, oracle_lib):
     assert r.ret == -1 and r.first_bad == first
     assert r.status[bad_at] == 1 and r.status[first] == 1 and r.status.count(0) == n - 2
     assert r.out[:4096 * 96] == ark and r.out[bad_at * 96:(bad_at + 1) * 96] == bytes(96)
+
+
+@pytest.mark.parametrize("n", [(1 << 18), (1 << 18) + 1, 3 * (1 << 17) + 5, (1 << 24) + 3])
+def test_host_chunk_schedule_boundaries(gpu, oracle_lib, n):
+    """run_host's chunk schedule (csrc/capi.hip): up to 2^18 points one chunk; above, >= 8 chunks of
+    >= 2^17 points (multiples of 256) up to 2^21 — here 1, 3, 4 and 9 chunks, the last a ragged
+    1 / 5 / 3 points. A bad point in the middle and one in the very last record: first_bad is the
+    middle one, each status lands at its global index, every other record is the oracle's."""
+    base, ark = _random_stream(oracle_lib, 4096, seed=11)
+    reps = -(-n // 4096)
+    data = bytearray((base * reps)[:n * 48])
+    mid, last = n // 2 + 3, n - 1
+    data[mid * 48] &= 0x7F
+    data[last * 48] &= 0x7F
+    r = gpu.g1_decompress(bytes(data), want_status=True)
+    assert r.ret == -1 and r.first_bad == mid
+    assert r.status[mid] == 1 and r.status[last] == 1 and r.status.count(0) == n - 2
+    want = bytearray((ark * reps)[:n * 96])
+    want[mid * 96:(mid + 1) * 96] = bytes(96)
+    want[last * 96:(last + 1) * 96] = bytes(96)
+    assert r.out == bytes(want)
 
 
 def test_transcript_config1(gpu):

@@ -1,0 +1,77 @@
+"""CPU checks of the measurement tools whose output is committed under profiles/: the e2e stage
+summary (tools/stage_summary.py) on a synthetic three-trace run, and the fetch-probe summary's
+request-size arithmetic (tools/fetch_probe_summary.py). No GPU."""
+import csv
+import json
+import os
+import subprocess
+import sys
+
+from conftest import ROOT
+
+TOOLS = os.path.join(ROOT, "tools")
+
+
+def write_csv(path, header, rows):
+    with open(path, "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(header)
+        w.writerows(rows)
+
+
+def test_stage_summary_critical_path_adds_up(tmp_path):
+    ms = 1_000_000
+    mk = [("kzgpot.preprocess", 1, 0, 5 * ms),  # the warm-up call (skipped)
+          ("kzgpot.preprocess_file", 1, 9 * ms, 130 * ms),
+          ("kzgpot.preprocess", 1, 10 * ms, 110 * ms),
+          ("kzgpot.section.tau_g1", 2, 11 * ms, 40 * ms),
+          ("kzgpot.section.tau_g2", 2, 41 * ms, 60 * ms),
+          ("kzgpot.h2d", 2, 11 * ms, 12 * ms),
+          ("kzgpot.blake2b.output", 3, 20 * ms, 109 * ms),
+          ("kzgpot.file_finish", 1, 111 * ms, 112 * ms)]
+    write_csv(tmp_path / "run_marker_api_trace.csv",
+              ["Domain", "Function", "Process_Id", "Thread_Id", "Correlation_Id", "Start_Timestamp", "End_Timestamp"],
+              [["MARKER_CORE_RANGE_API", n, 1, t, i, a, b] for i, (n, t, a, b) in enumerate(mk)])
+    write_csv(tmp_path / "run_kernel_trace.csv", ["Kernel_Name", "Start_Timestamp", "End_Timestamp"],
+              [["kzgpot::k_g1_codec(x)", 12 * ms, 30 * ms], ["kzgpot::k_g2_codec(x)", 42 * ms, 58 * ms]])
+    write_csv(tmp_path / "run_memory_copy_trace.csv", ["Direction", "Start_Timestamp", "End_Timestamp"],
+              [["MEMORY_COPY_HOST_TO_DEVICE", 11 * ms, 12 * ms], ["MEMORY_COPY_DEVICE_TO_HOST", 30 * ms, 32 * ms]])
+    calls = tmp_path / "calls.json"
+    calls.write_text(json.dumps({"n_log2": 21, "shards": 1, "blake2b_transcript_alone_s": 0.35,
+                                 "calls": [{"call": "kgz_file_digests", "seconds": 0.121, "rc": 0}]}))
+    p = subprocess.run([sys.executable, os.path.join(TOOLS, "stage_summary.py"), str(tmp_path), str(calls)],
+                       capture_output=True, text=True, check=True)
+    (c,) = json.loads(p.stdout)["calls"]
+    assert c["range_ms"] == 100.0 and c["critical_path_sum_ms"] == 100.0
+    assert [n for n, _ in c["critical_path_ms"]] == ["setup", "section.tau_g1", "between sections", "section.tau_g2",
+                                                   "after the last section (digest / writer drain)"]
+    assert c["critical_path_ms"][-1][1] == 50.0
+    assert c["last_to_finish"] == "kzgpot.blake2b.output"
+    assert c["busy_ms"]["gpu.kernels"] == 34.0 and c["busy_ms"]["gpu.copy.d2h"] == 2.0
+    assert c["file"]["file_call_ms"] == 121.0 and c["file"]["after_pipeline_ms"] == 20.0
+
+
+def test_fetch_probe_summary_splits_request_sizes(tmp_path):
+    """128-B data requests vs 64-B instruction-fetch requests: bytes_by_size counts each at its size,
+    while FETCH_SIZE (every request at 64 B) x 2 over-counts the 64-B ones."""
+    n = 1 << 20
+    name = "kzgpot::k_g2_codec(x)"
+    d = tmp_path / "lib1"
+    for sub, counters in (("FETCH_SIZE", {"FETCH_SIZE": (786440 + 72077) * 64 / 1024}),
+                          ("WRITE_SIZE", {"WRITE_SIZE": 192 * n / 1024}),
+                          ("SQC_ICACHE_MISSES", {"SQC_ICACHE_MISSES": 1.5 * n, "SQ_INSTS_VALU": 952781 * n / 64,
+                                                 "SQ_WAVES": n / 64}),
+                          ("TCC_EA0_RDREQ_sum", {"TCC_EA0_RDREQ_sum": 786440 + 72077, "TCC_EA0_RDREQ_32B_sum": 0,
+                                                 "TCC_EA0_RDREQ_128B_sum": 786440, "TCC_EA0_RDREQ_DRAM_sum": 858517,
+                                                 "SQC_TC_INST_REQ": 8.5e7, "SQC_TC_DATA_READ_REQ": 864})):
+        os.makedirs(d / sub)
+        write_csv(d / sub / "run_counter_collection.csv", ["Dispatch_Id", "Grid_Size", "Kernel_Name", "Counter_Name",
+                                                            "Counter_Value"],
+                  [[7, n, name, k, v] for k, v in counters.items()])
+    (tmp_path / "lib1.name").write_text("build/libkzgpot.so\n")
+    p = subprocess.run([sys.executable, os.path.join(TOOLS, "fetch_probe_summary.py"), str(tmp_path)],
+                       capture_output=True, text=True, check=True)
+    row = json.loads(p.stdout)["builds"]["build/libkzgpot.so"][f"k_g2_codec @ {n}"]
+    assert abs(row["rdreq"]["bytes_by_size_per_point"] - (786440 * 128 + 72077 * 64) / n) < 1e-3
+    assert row["rdreq"]["64B"] == 72077 and row["write_B_per_point"] == 192.0
+    assert row["fetch_B_per_point"] > row["rdreq"]["bytes_by_size_per_point"]  # the x2 correction's over-count

@@ -111,6 +111,16 @@ def main():
             t = max(t, b)
         path.append(["after the last section (digest / writer drain)", (e - t) / 1e6])
         enders = sorted(((m[3], m[0]) for m in inside if m[3] <= e), reverse=True)
+        # file calls: kzgpot_preprocess_ex's own range around preprocess_impl (open + mapping the
+        # buffers before it; closing, renaming and unmapping after it)
+        outer = [m for m in markers if m[0] == "kzgpot.preprocess_file" and m[2] <= s and m[3] >= e]
+        file_part = None
+        if outer:
+            o = outer[0]
+            fin = [m for m in markers if m[0] == "kzgpot.file_finish" and o[2] <= m[2] <= o[3]]
+            file_part = {"file_call_ms": (o[3] - o[2]) / 1e6, "before_pipeline_ms": (s - o[2]) / 1e6,
+                         "after_pipeline_ms": (o[3] - e) / 1e6,
+                         "file_finish_ms": sum(m[3] - m[2] for m in fin) / 1e6}
         out["calls"].append({
             "call": call["call"], "seconds_timed_by_caller": call["seconds"], "rc": call["rc"],
             "range_ms": (e - s) / 1e6,
@@ -119,6 +129,7 @@ def main():
             "busy_ms": busy, "kernel_ms": {k: round(v, 3) for k, v in sorted(per_kernel.items(), key=lambda kv: -kv[1])},
             "last_to_finish": enders[0][1] if enders else None,
             "last_to_finish_before_end_ms": round((e - enders[0][0]) / 1e6, 3) if enders else None,
+            "file": file_part,
         })
     print(json.dumps(out, indent=1))
 
