@@ -117,3 +117,42 @@ def test_current_device_is_restored(gpu):
     gpu.preprocess_buffer(bytes(_tr()), 10, n_gpus=3)
     assert gpu.g1_decompress(bytes(48)).ret == -1  # a rejected point: the error path through run_host
     assert torch.cuda.current_device() == before
+
+
+def _synth_transcript(n_log2, seed):
+    """A response-layout transcript of GPU-generated valid points (as bench.py's e2e rows) plus the
+    generator's expected ark bytes of τG1 and ατG1."""
+    import torch
+    from kzgpot import device as D
+
+    dev = torch.device("cuda", 0)
+    n = 1 << n_log2
+    parts, expect = [torch.zeros(64, dtype=torch.uint8, device=dev)], {}
+    for k, (name, kind, cnt) in enumerate((("tau_g1", "g1", 2 * n - 1), ("tau_g2", "g2", n), ("alpha_g1", "g1", n),
+                                           ("beta_g1", "g1", n), ("beta_g2", "g2", 1))):
+        c, e = D.synth(kind, seed + k, 0, cnt, dev, with_expected=name in ("tau_g1", "alpha_g1"))
+        parts.append(c)
+        if e is not None:
+            expect[name] = bytes(e.cpu().numpy())
+    parts.append(torch.zeros(3 * 192 + 6 * 96, dtype=torch.uint8, device=dev))
+    return bytearray(torch.cat(parts).cpu().numpy()), expect
+
+
+@pytest.mark.parametrize("mode", [0, 1], ids=["kgz", "fastkgz"])
+def test_streamed_digest_with_small_first_chunk(gpu, mode):
+    """N = 2^18: τG1 (2^19 - 1 points) and ατG1 run in several host chunks, and with the output
+    digest streaming from them the first chunk is the small 2^16-point one (csrc/capi.hip
+    run_host). Both digests equal hashlib's over the same bytes, τG1 / ατG1 equal the generator's;
+    then bad points in that first chunk and in a later one: the first chunk's is reported."""
+    n_log2, n = 18, 1 << 18
+    tr, expect = _synth_transcript(n_log2, seed=71 + mode)
+    res = gpu.preprocess_buffer(bytes(tr), n_log2, mode, n_gpus=1, with_digests=True)
+    g1n = (2 * n - 1) * 96
+    assert res.out[:g1n] == expect["tau_g1"] and res.out[g1n:g1n + n * 96] == expect["alpha_g1"]
+    assert res.transcript_digest == hashlib.blake2b(bytes(tr)).hexdigest()
+    assert res.output_digest == hashlib.blake2b(res.out).hexdigest()
+    for i in ((1 << 16) - 1, 3 * (1 << 17) + 9):
+        tr[64 + i * 48] &= 0x7F  # compression bit cleared: UnexpectedCompressionMode
+    with pytest.raises(gpu.KzgPotError) as e:
+        gpu.preprocess_buffer(bytes(tr), n_log2, mode, n_gpus=1, with_digests=True)
+    assert (e.value.code, e.value.section, e.value.first_bad) == (-1, 0, (1 << 16) - 1)
