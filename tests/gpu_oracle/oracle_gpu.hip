@@ -1,0 +1,775 @@
+// TEST-ONLY GPU checker: the C oracle's per-point algorithms (oracle/kzgpot_ref.c) and the Python
+// oracle's BN254 decompression (oracle/kzgpot_oracle.py bn254_g1_decompress_point), restated as
+// device code, so that a full-size output of the product kernels (2^27 G1 for config 4, 2^20 G2 for
+// config 3, 2^28 BN254 for config 5) can be re-derived point by point by an implementation that
+// shares nothing with kzg-setup-powersoftau_amd/csrc: 6 (BLS12-381) / 4 (BN254) x 64-bit limbs,
+// ark-ff's CIOS Montgomery multiply with R = 2^384 / 2^256, the reference's own algorithms
+// (pairing 0.14.2 Fq::sqrt a^((p-3)/4) by bit-serial square-and-multiply, Fq2::sqrt Algorithm 9,
+// ark-ec 0.2 mul_bits(r) with double_in_place / add_assign_mixed for the subgroup check), byte-level
+// record parsing. The C oracle runs ~4-60 K points/s on 16 cores, too slow for 2^27; this port runs
+// the same functions one point per lane. tests/test_gpu_oracle_port.py first checks it against the
+// C / Python oracles on every golden vector and on mixed random streams, then uses it at full size.
+//
+// Only tests/ load this library (tests/gpu_oracle/build/liboracle_gpu.so). The product never does.
+// Each function below names the oracle function it restates (kzgpot_ref.c line).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace og {
+
+#define OD __device__ __forceinline__
+
+// ------------------------------------------------------------------------------------ fields
+struct Bls {  // BLS12-381 Fq (kzgpot_ref.c:35-44)
+  static constexpr int N = 6;
+};
+struct Bn {  // BN254 Fq (kzgpot_oracle.py:592)
+  static constexpr int N = 4;
+};
+__constant__ uint64_t BLS_P[6] = {0xb9feffffffffaaabull, 0x1eabfffeb153ffffull, 0x6730d2a0f6b0f624ull,
+                                  0x64774b84f38512bfull, 0x4b1ba7b6434bacd7ull, 0x1a0111ea397fe69aull};
+__constant__ uint64_t BLS_R2[6] = {0xf4df1f341c341746ull, 0x0a76e6a609d104f1ull, 0x8de5476c4c95b6d5ull,
+                                   0x67eb88a9939d83c0ull, 0x9a793e85b519952dull, 0x11988fe592cae3aaull};
+__constant__ uint64_t BLS_ONE[6] = {0x760900000002fffdull, 0xebf4000bc40c0002ull, 0x5f48985753c758baull,
+                                    0x77ce585370525745ull, 0x5c071a97a256ec6dull, 0x15f65ec3fa80e493ull};
+__constant__ uint64_t BLS_PM3_4[6] = {0xee7fbfffffffeaaaull, 0x07aaffffac54ffffull, 0xd9cc34a83dac3d89ull,
+                                      0xd91dd2e13ce144afull, 0x92c6e9ed90d2eb35ull, 0x0680447a8e5ff9a6ull};
+__constant__ uint64_t BLS_PM1_2[6] = {0xdcff7fffffffd555ull, 0x0f55ffff58a9ffffull, 0xb39869507b587b12ull,
+                                      0xb23ba5c279c2895full, 0x258dd3db21a5d66bull, 0x0d0088f51cbff34dull};
+__constant__ uint64_t RORD[4] = {0xffffffff00000001ull, 0x53bda402fffe5bfeull, 0x3339d80809a1d805ull,
+                                 0x73eda753299d7d48ull};
+__constant__ uint64_t BN_P[4] = {0x3c208c16d87cfd47ull, 0x97816a916871ca8dull, 0xb85045b68181585dull,
+                                 0x30644e72e131a029ull};
+__constant__ uint64_t BN_R2[4] = {0xf32cfc5b538afa89ull, 0xb5e71911d44501fbull, 0x47ab1eff0a417ff6ull,
+                                  0x06d89f71cab8351full};
+__constant__ uint64_t BN_ONE[4] = {0xd35d438dc58f0d9dull, 0x0a78eb28f5c70b3dull, 0x666ea36f7879462cull,
+                                   0x0e0a77c19a07df2full};
+__constant__ uint64_t BN_PP1_4[4] = {0x4f082305b61f3f52ull, 0x65e05aa45a1c72a3ull, 0x6e14116da0605617ull,
+                                     0x0c19139cb84c680aull};
+constexpr uint64_t BLS_INV = 0x89f3fffcfffcfffdull;  // -p^-1 mod 2^64
+constexpr uint64_t BN_INV = 0x87d20782e4866389ull;
+
+template <class T> OD const uint64_t* P();
+template <> OD const uint64_t* P<Bls>() { return BLS_P; }
+template <> OD const uint64_t* P<Bn>() { return BN_P; }
+template <class T> OD const uint64_t* R2();
+template <> OD const uint64_t* R2<Bls>() { return BLS_R2; }
+template <> OD const uint64_t* R2<Bn>() { return BN_R2; }
+template <class T> OD const uint64_t* ONE();
+template <> OD const uint64_t* ONE<Bls>() { return BLS_ONE; }
+template <> OD const uint64_t* ONE<Bn>() { return BN_ONE; }
+template <class T> constexpr uint64_t INV();
+template <> constexpr uint64_t INV<Bls>() { return BLS_INV; }
+template <> constexpr uint64_t INV<Bn>() { return BN_INV; }
+
+template <class T>
+struct fp {
+  uint64_t l[T::N];
+};
+
+// (hi, lo) = a b + t + c: the C oracle's `u128 s = (u128)a * b + t + c`
+OD void mac(uint64_t a, uint64_t b, uint64_t t, uint64_t c, uint64_t& lo, uint64_t& hi) {
+  uint64_t x = a * b, h = __umul64hi(a, b);
+  x += t;
+  h += x < t;
+  x += c;
+  h += x < c;
+  lo = x;
+  hi = h;
+}
+
+template <class T>
+OD bool geq_p(const uint64_t* a) {  // fp_geq_p, kzgpot_ref.c:47
+  for (int i = T::N - 1; i >= 0; i--) {
+    if (a[i] > P<T>()[i]) return true;
+    if (a[i] < P<T>()[i]) return false;
+  }
+  return true;
+}
+template <class T>
+OD void sub_p(uint64_t* a) {  // sub_p, kzgpot_ref.c:54
+  uint64_t br = 0;
+  for (int i = 0; i < T::N; i++) {
+    const uint64_t pi = P<T>()[i];
+    const uint64_t d = a[i] - pi - br;
+    br = (a[i] < pi) || (a[i] - pi < br);
+    a[i] = d;
+  }
+}
+template <class T>
+OD void f_add(fp<T>& r, const fp<T>& a, const fp<T>& b) {  // fp_add, kzgpot_ref.c:62
+  uint64_t c = 0;
+  for (int i = 0; i < T::N; i++) {
+    const uint64_t s = a.l[i] + b.l[i];
+    const uint64_t s2 = s + c;
+    c = (s < a.l[i]) || (s2 < s);
+    r.l[i] = s2;
+  }
+  if (geq_p<T>(r.l)) sub_p<T>(r.l);
+}
+template <class T>
+OD void f_sub(fp<T>& r, const fp<T>& a, const fp<T>& b) {  // fp_sub, kzgpot_ref.c:71
+  uint64_t br = 0, t[T::N];
+  for (int i = 0; i < T::N; i++) {
+    const uint64_t d = a.l[i] - b.l[i] - br;
+    br = (a.l[i] < b.l[i]) || (a.l[i] - b.l[i] < br);
+    t[i] = d;
+  }
+  if (br) {
+    uint64_t c = 0;
+    for (int i = 0; i < T::N; i++) {
+      const uint64_t s = t[i] + P<T>()[i];
+      const uint64_t s2 = s + c;
+      c = (s < t[i]) || (s2 < s);
+      t[i] = s2;
+    }
+  }
+  for (int i = 0; i < T::N; i++) r.l[i] = t[i];
+}
+template <class T>
+OD void f_dbl(fp<T>& r, const fp<T>& a) { f_add<T>(r, a, a); }
+template <class T>
+OD void f_zero(fp<T>& r) {
+  for (int i = 0; i < T::N; i++) r.l[i] = 0;
+}
+template <class T>
+OD void f_one(fp<T>& r) {
+  for (int i = 0; i < T::N; i++) r.l[i] = ONE<T>()[i];
+}
+template <class T>
+OD void f_neg(fp<T>& r, const fp<T>& a) {  // fp_neg, kzgpot_ref.c:90
+  fp<T> z;
+  f_zero<T>(z);
+  f_sub<T>(r, z, a);
+}
+// CIOS Montgomery multiply, ark-ff 0.2 (fp_mul, kzgpot_ref.c:94-120)
+template <class T>
+__device__ void f_mul(fp<T>& r, const fp<T>& a, const fp<T>& b) {
+  constexpr int N = T::N;
+  uint64_t t[N + 2];
+  for (int j = 0; j < N + 2; j++) t[j] = 0;
+  for (int i = 0; i < N; i++) {
+    uint64_t c = 0;
+    for (int j = 0; j < N; j++) mac(a.l[j], b.l[i], t[j], c, t[j], c);
+    uint64_t s = t[N] + c;
+    t[N + 1] = s < c;
+    t[N] = s;
+    const uint64_t m = t[0] * INV<T>();
+    uint64_t lo;
+    mac(m, P<T>()[0], t[0], 0, lo, c);
+    for (int j = 1; j < N; j++) mac(m, P<T>()[j], t[j], c, t[j - 1], c);
+    s = t[N] + c;
+    t[N - 1] = s;
+    t[N] = t[N + 1] + (s < c);
+  }
+  for (int i = 0; i < N; i++) r.l[i] = t[i];
+  if (geq_p<T>(r.l)) sub_p<T>(r.l);
+}
+template <class T>
+OD void f_sqr(fp<T>& r, const fp<T>& a) { f_mul<T>(r, a, a); }
+template <class T>
+OD bool f_is_zero(const fp<T>& a) {
+  uint64_t o = 0;
+  for (int i = 0; i < T::N; i++) o |= a.l[i];
+  return o == 0;
+}
+template <class T>
+OD bool f_eq(const fp<T>& a, const fp<T>& b) {
+  for (int i = 0; i < T::N; i++)
+    if (a.l[i] != b.l[i]) return false;
+  return true;
+}
+template <class T>
+OD void f_from_canon(fp<T>& r, const uint64_t* c) {  // fp_from_canon, kzgpot_ref.c:127
+  fp<T> a, b;
+  for (int i = 0; i < T::N; i++) a.l[i] = c[i], b.l[i] = R2<T>()[i];
+  f_mul<T>(r, a, b);
+}
+template <class T>
+OD void f_to_canon(uint64_t* c, const fp<T>& a) {  // fp_to_canon, kzgpot_ref.c:133
+  fp<T> one, t;
+  f_zero<T>(one);
+  one.l[0] = 1;
+  f_mul<T>(t, a, one);
+  for (int i = 0; i < T::N; i++) c[i] = t.l[i];
+}
+// MSB-first square-and-multiply over a little-endian exponent (fp_pow, kzgpot_ref.c:139)
+template <class T>
+__device__ void f_pow(fp<T>& r, const fp<T>& a, const uint64_t* e) {
+  fp<T> res;
+  f_one<T>(res);
+  bool started = false;
+  for (int i = T::N - 1; i >= 0; i--)
+    for (int b = 63; b >= 0; b--) {
+      if (started) f_sqr<T>(res, res);
+      if ((e[i] >> b) & 1) {
+        f_mul<T>(res, res, a);
+        started = true;
+      }
+    }
+  r = res;
+}
+template <class T>
+OD int cmp_canon(const uint64_t* a, const uint64_t* b) {  // kzgpot_ref.c:164
+  for (int i = T::N - 1; i >= 0; i--) {
+    if (a[i] < b[i]) return -1;
+    if (a[i] > b[i]) return 1;
+  }
+  return 0;
+}
+template <class T>
+OD bool f_lt(const fp<T>& a, const fp<T>& b) {  // fp_lt, kzgpot_ref.c:172
+  uint64_t ca[T::N], cb[T::N];
+  f_to_canon<T>(ca, a);
+  f_to_canon<T>(cb, b);
+  return cmp_canon<T>(ca, cb) < 0;
+}
+using Fq = fp<Bls>;
+// pairing 0.14.2 Fq::sqrt (fq_sqrt, kzgpot_ref.c:179)
+OD bool fq_sqrt(Fq& r, const Fq& a) {
+  Fq a1, a0, neg1, one;
+  f_pow<Bls>(a1, a, BLS_PM3_4);
+  f_sqr<Bls>(a0, a1);
+  f_mul<Bls>(a0, a0, a);
+  f_one<Bls>(one);
+  f_neg<Bls>(neg1, one);
+  if (f_eq<Bls>(a0, neg1)) return false;
+  f_mul<Bls>(r, a1, a);
+  return true;
+}
+
+// ------------------------------------------------------------------------------------ Fq2
+struct Fq2 {
+  Fq c0, c1;
+};
+OD void f_add(Fq2& r, const Fq2& a, const Fq2& b) { f_add<Bls>(r.c0, a.c0, b.c0), f_add<Bls>(r.c1, a.c1, b.c1); }
+OD void f_sub(Fq2& r, const Fq2& a, const Fq2& b) { f_sub<Bls>(r.c0, a.c0, b.c0), f_sub<Bls>(r.c1, a.c1, b.c1); }
+OD void f_dbl(Fq2& r, const Fq2& a) { f_add(r, a, a); }
+OD void f_neg(Fq2& r, const Fq2& a) { f_neg<Bls>(r.c0, a.c0), f_neg<Bls>(r.c1, a.c1); }
+__device__ void f_mul(Fq2& r, const Fq2& a, const Fq2& b) {  // fp2_mul, kzgpot_ref.c:194 (Karatsuba)
+  Fq aa, bb, s0, s1, t;
+  f_mul<Bls>(aa, a.c0, b.c0);
+  f_mul<Bls>(bb, a.c1, b.c1);
+  f_add<Bls>(s0, a.c0, a.c1);
+  f_add<Bls>(s1, b.c0, b.c1);
+  f_mul<Bls>(t, s0, s1);
+  f_sub<Bls>(t, t, aa);
+  f_sub<Bls>(r.c1, t, bb);
+  f_sub<Bls>(r.c0, aa, bb);
+}
+OD void f_sqr(Fq2& r, const Fq2& a) { f_mul(r, a, a); }
+OD bool f_is_zero(const Fq2& a) { return f_is_zero<Bls>(a.c0) && f_is_zero<Bls>(a.c1); }
+OD bool f_eq(const Fq2& a, const Fq2& b) { return f_eq<Bls>(a.c0, b.c0) && f_eq<Bls>(a.c1, b.c1); }
+OD void f_zero(Fq2& r) { f_zero<Bls>(r.c0), f_zero<Bls>(r.c1); }
+OD void f_one(Fq2& r) { f_one<Bls>(r.c0), f_zero<Bls>(r.c1); }
+__device__ void f2_pow(Fq2& r, const Fq2& a, const uint64_t* e) {  // fp2_pow, kzgpot_ref.c:208
+  Fq2 res;
+  f_one(res);
+  bool started = false;
+  for (int i = 5; i >= 0; i--)
+    for (int b = 63; b >= 0; b--) {
+      if (started) f_sqr(res, res);
+      if ((e[i] >> b) & 1) {
+        f_mul(res, res, a);
+        started = true;
+      }
+    }
+  r = res;
+}
+// pairing 0.14.2 Fq2::sqrt, Algorithm 9 (fq2_sqrt, kzgpot_ref.c:224)
+__device__ bool fq2_sqrt(Fq2& r, const Fq2& a) {
+  if (f_is_zero(a)) {
+    r = a;
+    return true;
+  }
+  Fq2 a1, alpha, a0, neg1, one;
+  f_one(one);
+  f_neg<Bls>(neg1.c0, one.c0);
+  f_zero<Bls>(neg1.c1);
+  f2_pow(a1, a, BLS_PM3_4);
+  f_sqr(alpha, a1);
+  f_mul(alpha, alpha, a);
+  a0 = alpha;
+  f_neg<Bls>(a0.c1, a0.c1);  // frobenius_map(1)
+  f_mul(a0, a0, alpha);
+  if (f_eq(a0, neg1)) return false;
+  f_mul(a1, a1, a);
+  if (f_eq(alpha, neg1)) {  // a1 u = (-a1.c1, a1.c0)
+    Fq2 t;
+    f_neg<Bls>(t.c0, a1.c1);
+    t.c1 = a1.c0;
+    r = t;
+  } else {
+    f_add(alpha, alpha, one);
+    f2_pow(alpha, alpha, BLS_PM1_2);
+    f_mul(r, a1, alpha);
+  }
+  return true;
+}
+OD bool f2_lt(const Fq2& a, const Fq2& b) {  // fp2_lt, kzgpot_ref.c:257 (lexicographic on c1, c0)
+  uint64_t a1[6], b1[6];
+  f_to_canon<Bls>(a1, a.c1);
+  f_to_canon<Bls>(b1, b.c1);
+  const int c = cmp_canon<Bls>(a1, b1);
+  if (c) return c < 0;
+  return f_lt<Bls>(a.c0, b.c0);
+}
+// uniform names for the curve template
+OD void f_add(Fq& r, const Fq& a, const Fq& b) { f_add<Bls>(r, a, b); }
+OD void f_sub(Fq& r, const Fq& a, const Fq& b) { f_sub<Bls>(r, a, b); }
+OD void f_dbl(Fq& r, const Fq& a) { f_dbl<Bls>(r, a); }
+OD void f_mul(Fq& r, const Fq& a, const Fq& b) { f_mul<Bls>(r, a, b); }
+OD void f_sqr(Fq& r, const Fq& a) { f_sqr<Bls>(r, a); }
+OD bool f_is_zero(const Fq& a) { return f_is_zero<Bls>(a); }
+OD bool f_eq(const Fq& a, const Fq& b) { return f_eq<Bls>(a, b); }
+OD void f_zero(Fq& r) { f_zero<Bls>(r); }
+OD void f_one(Fq& r) { f_one<Bls>(r); }
+
+// ------------------------------------------------------------------------------------ ark-ec 0.2 Jacobian
+template <class F>
+struct Jac {
+  F x, y, z;
+};
+// GroupProjective::double_in_place, COEFF_A == 0 (kzgpot_ref.c:270)
+template <class F>
+__device__ void jac_double(Jac<F>& p) {
+  if (f_is_zero(p.z)) return;
+  F a, b, c, d, e, f, t;
+  f_sqr(a, p.x);
+  f_sqr(b, p.y);
+  f_sqr(c, b);
+  f_add(t, p.x, b);
+  f_sqr(t, t);
+  f_sub(t, t, a);
+  f_sub(t, t, c);
+  f_dbl(d, t);
+  f_dbl(e, a);
+  f_add(e, e, a);
+  f_sqr(f, e);
+  f_mul(p.z, p.z, p.y);
+  f_dbl(p.z, p.z);
+  f_sub(p.x, f, d);
+  f_sub(p.x, p.x, d);
+  f_dbl(c, c);
+  f_dbl(c, c);
+  f_dbl(c, c);
+  f_sub(t, d, p.x);
+  f_mul(t, t, e);
+  f_sub(p.y, t, c);
+}
+// GroupProjective::add_assign_mixed (kzgpot_ref.c:296)
+template <class F>
+__device__ void jac_add_mixed(Jac<F>& p, const F& x2, const F& y2, bool inf2) {
+  if (inf2) return;
+  if (f_is_zero(p.z)) {
+    p.x = x2;
+    p.y = y2;
+    f_one(p.z);
+    return;
+  }
+  F z1z1, u2, s2, h, hh, i, j, r, v, t;
+  f_sqr(z1z1, p.z);
+  f_mul(u2, x2, z1z1);
+  f_mul(s2, y2, p.z);
+  f_mul(s2, s2, z1z1);
+  if (f_eq(p.x, u2) && f_eq(p.y, s2)) {
+    jac_double(p);
+    return;
+  }
+  f_sub(h, u2, p.x);
+  f_sqr(hh, h);
+  f_dbl(i, hh);
+  f_dbl(i, i);
+  f_mul(j, h, i);
+  f_sub(r, s2, p.y);
+  f_dbl(r, r);
+  f_mul(v, p.x, i);
+  f_sqr(p.x, r);
+  f_sub(p.x, p.x, j);
+  f_sub(p.x, p.x, v);
+  f_sub(p.x, p.x, v);
+  f_mul(j, j, p.y);
+  f_dbl(j, j);
+  f_sub(t, v, p.x);
+  f_mul(t, t, r);
+  f_sub(p.y, t, j);
+  f_add(p.z, p.z, h);
+  f_sqr(p.z, p.z);
+  f_sub(p.z, p.z, z1z1);
+  f_sub(p.z, p.z, hh);
+}
+// GroupAffine::mul_bits(BitIteratorBE(r)).is_zero() (kzgpot_ref.c:336)
+template <class F>
+__device__ bool in_subgroup_ref(const F& x, const F& y, bool inf) {
+  Jac<F> acc;
+  f_zero(acc.x);
+  f_one(acc.y);
+  f_zero(acc.z);
+  bool started = false;
+  for (int w = 3; w >= 0; w--)
+    for (int b = 63; b >= 0; b--) {
+      const bool bit = (RORD[w] >> b) & 1;
+      if (!started && !bit) continue;
+      started = true;
+      jac_double(acc);
+      if (bit) jac_add_mixed(acc, x, y, inf);
+    }
+  return f_is_zero(acc.z);
+}
+
+// ------------------------------------------------------------------------------------ bytes
+template <int N>
+OD void be_to_limbs(uint64_t* c, const uint8_t* b) {  // be48_to_limbs, kzgpot_ref.c:357
+  for (int i = 0; i < N; i++) {
+    uint64_t v = 0;
+    for (int k = 0; k < 8; k++) v = (v << 8) | b[(N - 1 - i) * 8 + k];
+    c[i] = v;
+  }
+}
+template <int N>
+OD void le_to_limbs(uint64_t* c, const uint8_t* b) {  // le48_to_limbs, kzgpot_ref.c:364
+  for (int i = 0; i < N; i++) {
+    uint64_t v = 0;
+    for (int k = 7; k >= 0; k--) v = (v << 8) | b[i * 8 + k];
+    c[i] = v;
+  }
+}
+template <int N>
+OD void limbs_to_le(uint8_t* b, const uint64_t* c) {  // limbs_to_le48, kzgpot_ref.c:371
+  for (int i = 0; i < N; i++)
+    for (int k = 0; k < 8; k++) b[i * 8 + k] = (uint8_t)(c[i] >> (8 * k));
+}
+template <int N>
+OD void limbs_to_be(uint8_t* b, const uint64_t* c) {  // limbs_to_be48, kzgpot_ref.c:375
+  for (int i = 0; i < N; i++)
+    for (int k = 0; k < 8; k++) b[(N - 1 - i) * 8 + (7 - k)] = (uint8_t)(c[i] >> (8 * k));
+}
+template <class T>
+OD void f_to_le(uint8_t* b, const fp<T>& a) {
+  uint64_t c[T::N];
+  f_to_canon<T>(c, a);
+  limbs_to_le<T::N>(b, c);
+}
+OD void f_to_be48(uint8_t* b, const Fq& a) {
+  uint64_t c[6];
+  f_to_canon<Bls>(c, a);
+  limbs_to_be<6>(b, c);
+}
+
+enum { ST_OK = 0, ST_COMPRESSION_MODE = 1, ST_UNEXPECTED_INFO = 2, ST_NOT_IN_FIELD = 3, ST_NOT_ON_CURVE = 4,
+       ST_NOT_IN_SUBGROUP = 5, ST_UNEXPECTED_FLAGS = 6, ST_INFINITY = 7 };
+constexpr uint32_t F_NO_SUBGROUP_CHECK = 0x1u;
+
+struct G1a {
+  Fq x, y;
+  bool inf;
+};
+struct G2a {
+  Fq2 x, y;
+  bool inf;
+};
+
+// G1Compressed::into_affine_unchecked (pairing_g1_decompress, kzgpot_ref.c:400)
+__device__ int pairing_g1_decompress(G1a& out, const uint8_t* enc) {
+  uint8_t copy[48];
+  for (int i = 0; i < 48; i++) copy[i] = enc[i];
+  if (!(copy[0] & 0x80)) return ST_COMPRESSION_MODE;
+  if (copy[0] & 0x40) {
+    copy[0] &= 0x3f;
+    for (int i = 0; i < 48; i++)
+      if (copy[i]) return ST_UNEXPECTED_INFO;
+    out.inf = true;
+    return ST_OK;
+  }
+  const bool greatest = (copy[0] & 0x20) != 0;
+  copy[0] &= 0x1f;
+  uint64_t c[6];
+  be_to_limbs<6>(c, copy);
+  if (geq_p<Bls>(c)) return ST_NOT_IN_FIELD;
+  Fq x, x3b, y, negy, b4;
+  f_from_canon<Bls>(x, c);
+  const uint64_t four[6] = {4, 0, 0, 0, 0, 0};
+  f_from_canon<Bls>(b4, four);
+  f_sqr(x3b, x);
+  f_mul(x3b, x3b, x);
+  f_add(x3b, x3b, b4);
+  if (!fq_sqrt(y, x3b)) return ST_NOT_ON_CURVE;
+  f_neg<Bls>(negy, y);
+  out.x = x;
+  out.y = (f_lt<Bls>(y, negy) ^ greatest) ? y : negy;
+  out.inf = false;
+  return ST_OK;
+}
+// G2Compressed::into_affine_unchecked (pairing_g2_decompress, kzgpot_ref.c:431)
+__device__ int pairing_g2_decompress(G2a& out, const uint8_t* enc) {
+  uint8_t copy[96];
+  for (int i = 0; i < 96; i++) copy[i] = enc[i];
+  if (!(copy[0] & 0x80)) return ST_COMPRESSION_MODE;
+  if (copy[0] & 0x40) {
+    copy[0] &= 0x3f;
+    for (int i = 0; i < 96; i++)
+      if (copy[i]) return ST_UNEXPECTED_INFO;
+    out.inf = true;
+    return ST_OK;
+  }
+  const bool greatest = (copy[0] & 0x20) != 0;
+  copy[0] &= 0x1f;
+  uint64_t c1[6], c0[6];
+  be_to_limbs<6>(c1, copy);
+  be_to_limbs<6>(c0, copy + 48);
+  if (geq_p<Bls>(c0) || geq_p<Bls>(c1)) return ST_NOT_IN_FIELD;
+  Fq2 x, x3b, y, negy, b;
+  f_from_canon<Bls>(x.c0, c0);
+  f_from_canon<Bls>(x.c1, c1);
+  const uint64_t four[6] = {4, 0, 0, 0, 0, 0};
+  f_from_canon<Bls>(b.c0, four);
+  b.c1 = b.c0;
+  f_sqr(x3b, x);
+  f_mul(x3b, x3b, x);
+  f_add(x3b, x3b, b);
+  if (!fq2_sqrt(y, x3b)) return ST_NOT_ON_CURVE;
+  f_neg(negy, y);
+  out.x = x;
+  out.y = (f2_lt(y, negy) ^ greatest) ? y : negy;
+  out.inf = false;
+  return ST_OK;
+}
+// pairing uncompressed encodings (kzgpot_ref.c:465, 474)
+OD void pairing_g1_uncompressed(uint8_t* b, const G1a& p) {
+  for (int i = 0; i < 96; i++) b[i] = 0;
+  if (p.inf) {
+    b[0] = 0x40;
+    return;
+  }
+  f_to_be48(b, p.x);
+  f_to_be48(b + 48, p.y);
+}
+OD void pairing_g2_uncompressed(uint8_t* b, const G2a& p) {
+  for (int i = 0; i < 192; i++) b[i] = 0;
+  if (p.inf) {
+    b[0] = 0x40;
+    return;
+  }
+  f_to_be48(b, p.x.c1);
+  f_to_be48(b + 48, p.x.c0);
+  f_to_be48(b + 96, p.y.c1);
+  f_to_be48(b + 144, p.y.c0);
+}
+// Fp384 deserialize(_with_flags) (ark_fp_read, kzgpot_ref.c:488)
+__device__ int ark_fp_read(Fq& r, const uint8_t* le, bool with_flags, bool* inf) {
+  uint8_t b[48];
+  for (int i = 0; i < 48; i++) b[i] = le[i];
+  if (with_flags) {
+    const bool pos = (b[47] >> 7) & 1, isinf = (b[47] >> 6) & 1;
+    if (pos && isinf) return ST_UNEXPECTED_FLAGS;
+    *inf = isinf;
+    b[47] &= 0x3f;
+  }
+  uint64_t c[6];
+  le_to_limbs<6>(c, b);
+  if (geq_p<Bls>(c)) return ST_NOT_IN_FIELD;
+  f_from_canon<Bls>(r, c);
+  return ST_OK;
+}
+// read_g1 (src/lib.rs:41-54) + deserialize_uncompressed (read_g1, kzgpot_ref.c:504)
+__device__ int read_g1(G1a& a, const uint8_t* pairing96, bool check) {
+  uint8_t ark[96];
+  for (int i = 0; i < 48; i++) {
+    ark[i] = pairing96[47 - i];
+    ark[48 + i] = pairing96[95 - i];
+  }
+  bool inf = false;
+  int st;
+  if ((st = ark_fp_read(a.x, ark, false, nullptr))) return st;
+  if ((st = ark_fp_read(a.y, ark + 48, true, &inf))) return st;
+  a.inf = inf;
+  if (check && !in_subgroup_ref<Fq>(a.x, a.y, inf)) return ST_NOT_IN_SUBGROUP;
+  return ST_OK;
+}
+// read_g2 (src/lib.rs:56-80) (read_g2, kzgpot_ref.c:523)
+__device__ int read_g2(G2a& a, const uint8_t* p, bool check) {
+  uint8_t ark[192];
+  const int src[4] = {48, 0, 144, 96};
+  for (int q = 0; q < 4; q++)
+    for (int i = 0; i < 48; i++) ark[q * 48 + i] = p[src[q] + 47 - i];
+  bool inf = false;
+  int st;
+  if ((st = ark_fp_read(a.x.c0, ark, false, nullptr))) return st;
+  if ((st = ark_fp_read(a.x.c1, ark + 48, false, nullptr))) return st;
+  if ((st = ark_fp_read(a.y.c0, ark + 96, false, nullptr))) return st;
+  if ((st = ark_fp_read(a.y.c1, ark + 144, true, &inf))) return st;
+  a.inf = inf;
+  if (check && !in_subgroup_ref<Fq2>(a.x, a.y, inf)) return ST_NOT_IN_SUBGROUP;
+  return ST_OK;
+}
+// serialize_uncompressed (kzgpot_ref.c:545, 550)
+OD void ark_g1_serialize(uint8_t* b, const G1a& a) {
+  f_to_le<Bls>(b, a.x);
+  f_to_le<Bls>(b + 48, a.y);
+  if (a.inf) b[95] |= 0x40;
+}
+OD void ark_g2_serialize(uint8_t* b, const G2a& a) {
+  f_to_le<Bls>(b, a.x.c0);
+  f_to_le<Bls>(b + 48, a.x.c1);
+  f_to_le<Bls>(b + 96, a.y.c0);
+  f_to_le<Bls>(b + 144, a.y.c1);
+  if (a.inf) b[191] |= 0x40;
+}
+// the check + emit stage (stage_check_g1 / _g2, kzgpot_ref.c:567, 581)
+__device__ int stage_check_g1(uint8_t* out, const G1a& p, uint32_t flags) {
+  G1a a;
+  if (flags & F_NO_SUBGROUP_CHECK) {
+    if (p.inf) {
+      f_zero(a.x);
+      f_one(a.y);
+      a.inf = true;
+    } else {
+      a = p;
+      a.inf = false;
+    }
+    ark_g1_serialize(out, a);
+    return ST_OK;
+  }
+  uint8_t un[96];
+  pairing_g1_uncompressed(un, p);
+  const int st = read_g1(a, un, true);
+  if (st) return p.inf ? ST_INFINITY : st;
+  ark_g1_serialize(out, a);
+  return ST_OK;
+}
+__device__ int stage_check_g2(uint8_t* out, const G2a& p, uint32_t flags) {
+  G2a a;
+  if (flags & F_NO_SUBGROUP_CHECK) {
+    if (p.inf) {
+      f_zero(a.x);
+      f_one(a.y);
+      a.inf = true;
+    } else {
+      a = p;
+      a.inf = false;
+    }
+    ark_g2_serialize(out, a);
+    return ST_OK;
+  }
+  uint8_t un[192];
+  pairing_g2_uncompressed(un, p);
+  const int st = read_g2(a, un, true);
+  if (st) return p.inf ? ST_INFINITY : st;
+  ark_g2_serialize(out, a);
+  return ST_OK;
+}
+
+// ark-bn254 0.2 G1Affine::deserialize (compressed) -> serialize_uncompressed
+// (kzgpot_oracle.py:645 bn254_g1_decompress_point)
+using Fb = fp<Bn>;
+__device__ int bn254_decompress(uint8_t* out64, const uint8_t* enc32) {
+  uint8_t b[32];
+  for (int i = 0; i < 32; i++) b[i] = enc32[i];
+  const uint8_t top = b[31];
+  const bool pos = (top >> 7) & 1, inf = (top >> 6) & 1;
+  if (pos && inf) return ST_UNEXPECTED_FLAGS;
+  b[31] &= 0x3f;
+  uint64_t xc[4];
+  le_to_limbs<4>(xc, b);
+  if (geq_p<Bn>(xc)) return ST_NOT_IN_FIELD;
+  if (inf) {  // zero(): x = 0, y = 1, infinity flag on y's top byte
+    for (int i = 0; i < 64; i++) out64[i] = 0;
+    out64[32] = 1;
+    out64[63] |= 0x40;
+    return ST_OK;
+  }
+  Fb x, rhs, three, y, y2, negy;
+  f_from_canon<Bn>(x, xc);
+  const uint64_t c3[4] = {3, 0, 0, 0};
+  f_from_canon<Bn>(three, c3);
+  f_sqr<Bn>(rhs, x);
+  f_mul<Bn>(rhs, rhs, x);
+  f_add<Bn>(rhs, rhs, three);  // x^3 + 3
+  f_pow<Bn>(y, rhs, BN_PP1_4);   // bn_sqrt: a^((p+1)/4), then y^2 == a
+  f_sqr<Bn>(y2, y);
+  if (!f_eq<Bn>(y2, rhs)) return ST_NOT_ON_CURVE;
+  f_neg<Bn>(negy, y);
+  const Fb& sel = (f_lt<Bn>(y, negy) ^ pos) ? y : negy;
+  uint64_t yc[4];
+  f_to_canon<Bn>(yc, sel);
+  limbs_to_le<4>(out64, xc);
+  limbs_to_le<4>(out64 + 32, yc);
+  return ST_OK;
+}
+
+// ------------------------------------------------------------------------------------ kernels
+// One lane = one point. Rejected records are zero-filled (finish, kzgpot_ref.c:655).
+__global__ void k_g1_decompress(const uint8_t* in, uint64_t n, uint8_t* out, uint8_t* status, uint32_t flags) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  G1a p;
+  int st = pairing_g1_decompress(p, in + 48 * i);
+  if (!st) st = stage_check_g1(out + 96 * i, p, flags);
+  if (st)
+    for (int k = 0; k < 96; k++) out[96 * i + k] = 0;
+  status[i] = (uint8_t)st;
+}
+__global__ void k_g2_decompress(const uint8_t* in, uint64_t n, uint8_t* out, uint8_t* status, uint32_t flags) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  G2a p;
+  int st = pairing_g2_decompress(p, in + 96 * i);
+  if (!st) st = stage_check_g2(out + 192 * i, p, flags);
+  if (st)
+    for (int k = 0; k < 192; k++) out[192 * i + k] = 0;
+  status[i] = (uint8_t)st;
+}
+__global__ void k_g1_transcode(const uint8_t* in, uint64_t n, uint8_t* out, uint8_t* status) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  G1a a;
+  const int st = read_g1(a, in + 96 * i, true);
+  if (!st) ark_g1_serialize(out + 96 * i, a);
+  else
+    for (int k = 0; k < 96; k++) out[96 * i + k] = 0;
+  status[i] = (uint8_t)st;
+}
+__global__ void k_g2_transcode(const uint8_t* in, uint64_t n, uint8_t* out, uint8_t* status) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  G2a a;
+  const int st = read_g2(a, in + 192 * i, true);
+  if (!st) ark_g2_serialize(out + 192 * i, a);
+  else
+    for (int k = 0; k < 192; k++) out[192 * i + k] = 0;
+  status[i] = (uint8_t)st;
+}
+__global__ void k_bn254_decompress(const uint8_t* in, uint64_t n, uint8_t* out, uint8_t* status) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int st = bn254_decompress(out + 64 * i, in + 32 * i);
+  if (st)
+    for (int k = 0; k < 64; k++) out[64 * i + k] = 0;
+  status[i] = (uint8_t)st;
+}
+
+}  // namespace og
+
+// ------------------------------------------------------------------------------------ C entry points
+// Device pointers, asynchronous on `stream`; status gets one byte per point (0 = accepted).
+// op: 0 G1 decompress (+ check unless flags & 1), 1 G2 decompress, 2 G1 transcode, 3 G2 transcode,
+// 4 BN254 decompress. Returns 0 or a hipError_t.
+extern "C" int oracle_gpu_run(int op, const void* d_in, uint64_t n, void* d_out, void* d_status, uint32_t flags,
+                              void* stream) {
+  if (n == 0) return 0;
+  constexpr unsigned kBlock = 64;
+  const dim3 grid((unsigned)((n + kBlock - 1) / kBlock)), block(kBlock);
+  hipStream_t s = (hipStream_t)stream;
+  const uint8_t* in = (const uint8_t*)d_in;
+  uint8_t* out = (uint8_t*)d_out;
+  uint8_t* st = (uint8_t*)d_status;
+  switch (op) {
+    case 0: hipLaunchKernelGGL(og::k_g1_decompress, grid, block, 0, s, in, n, out, st, flags); break;
+    case 1: hipLaunchKernelGGL(og::k_g2_decompress, grid, block, 0, s, in, n, out, st, flags); break;
+    case 2: hipLaunchKernelGGL(og::k_g1_transcode, grid, block, 0, s, in, n, out, st); break;
+    case 3: hipLaunchKernelGGL(og::k_g2_transcode, grid, block, 0, s, in, n, out, st); break;
+    case 4: hipLaunchKernelGGL(og::k_bn254_decompress, grid, block, 0, s, in, n, out, st); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  return (int)hipGetLastError();
+}

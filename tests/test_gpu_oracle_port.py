@@ -1,0 +1,197 @@
+"""Full-population independent parity at the BASELINE sizes (the 2^27 round
+trip compared the codec with a generator built from the same fp381.hpp / curve.hpp; only 16,640
+points of it were re-decoded by the C oracle).
+
+tests/gpu_oracle/oracle_gpu.hip restates the C oracle's per-point functions (oracle/kzgpot_ref.c:
+6 x 64-bit ark-ff CIOS, pairing's Fq::sqrt / Fq2::sqrt Algorithm 9, ark mul_bits(r), byte-level
+parsing) and the Python oracle's BN254 decompression as device code, sharing nothing with csrc/.
+First it is pinned to the oracles themselves — every golden vector and mixed random streams (valid,
+off-subgroup, non-residue, x >= p, flag damage) must give the C / Python oracle's bytes and
+statuses — then it re-derives EVERY point of config 4 (2^27 G1 + 2^16 G2), config 3's 2^20 G2,
+2^24 transcoded G1 records and config 5 (2^28 BN254), which the product kernels' output must equal
+byte for byte. Reference anchors: src/bin/preprocess-kgz.rs:105-110 (decompression),
+src/lib.rs:41-80 (read_g1 / read_g2), preprocess-kgz.rs:188-194 (serialize_uncompressed)."""
+import ctypes
+import os
+import random
+import subprocess
+
+import pytest
+
+from conftest import ROOT, golden, oracle_run
+
+pytestmark = pytest.mark.gpu
+
+PORT = os.path.join(ROOT, "tests", "gpu_oracle", "build", "liboracle_gpu.so")
+OPS = {"g1_decompress": (0, 48, 96), "g2_decompress": (1, 96, 192), "g1_transcode": (2, 96, 96),
+       "g2_transcode": (3, 192, 192), "bn254_g1_decompress": (4, 32, 64)}
+
+
+@pytest.fixture(scope="module")
+def port(gpu):
+    if not os.path.exists(PORT):
+        subprocess.run(["make", "-C", os.path.dirname(os.path.dirname(PORT))], check=True)
+    lib = ctypes.CDLL(PORT)
+    lib.oracle_gpu_run.restype = ctypes.c_int
+    lib.oracle_gpu_run.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+                                   ctypes.c_uint32, ctypes.c_void_p]
+    return lib
+
+
+def run_port(port, op, d_in, flags=0):
+    """The port over device bytes d_in: (out, status) device tensors."""
+    import torch
+
+    code, rin, rout = OPS[op]
+    n = d_in.numel() // rin
+    out = torch.full((max(1, n * rout),), 0x5A, dtype=torch.uint8, device=d_in.device)
+    st = torch.full((max(1, n),), 0xEE, dtype=torch.uint8, device=d_in.device)
+    rc = port.oracle_gpu_run(code, d_in.data_ptr(), n, out.data_ptr(), st.data_ptr(), flags,
+                             torch.cuda.current_stream().cuda_stream)
+    assert rc == 0, rc
+    torch.cuda.synchronize()
+    return out[:n * rout], st[:n]
+
+
+def port_host(port, op, data: bytes, flags=0):
+    import torch
+
+    d = torch.frombuffer(bytearray(data), dtype=torch.uint8).cuda()
+    out, st = run_port(port, op, d, flags)
+    return bytes(out.cpu().numpy()), bytes(st.cpu().numpy())
+
+
+# ------------------------------------------------------------------ the port against the oracles
+@pytest.mark.parametrize("op", ["g1_decompress", "g2_decompress", "g1_transcode", "g2_transcode"])
+@pytest.mark.parametrize("flags", [0, 1], ids=["checked", "unchecked"])
+def test_port_matches_c_oracle_on_golden_vectors(port, oracle_lib, op, flags):
+    if flags and "transcode" in op:
+        pytest.skip("the transcode path has no unchecked mode")
+    vecs = golden(op)  # every vector in both modes: the oracle defines the answer for any input
+    data = b"".join(bytes.fromhex(v["in"]) for v in vecs)
+    n = len(vecs)
+    out, st, _, _ = oracle_run(oracle_lib, op, data, n, flags=flags)
+    pout, pst = port_host(port, op, data, flags)
+    assert pst == st and pout == out
+
+
+def _mixed_g1(oracle_lib, n, seed):
+    """n compressed G1 points: multiples [k]G from the C oracle, with every 7th replaced by a
+    golden negative (off-subgroup, non-residue, x >= p, flags) and every 11th by random bytes with
+    the compression bit set (mostly non-residues or x >= p; on-curve ones are off-subgroup)."""
+    rng = random.Random(seed)
+    scal = b"".join(rng.randrange(1, 1 << 255).to_bytes(32, "big") for _ in range(n))
+    comp = ctypes.create_string_buffer(n * 48)
+    ark = ctypes.create_string_buffer(n * 96)
+    oracle_lib.oracle_g1_scalar_mul_encode(scal, ctypes.c_size_t(n), comp, ark)
+    data = bytearray(comp.raw)
+    negs = [bytes.fromhex(v["in"]) for v in golden("g1_decompress") if v["status"]]
+    for i in range(3, n, 7):
+        data[i * 48:(i + 1) * 48] = rng.choice(negs)
+    for i in range(5, n, 11):
+        r = bytearray(rng.randbytes(48))
+        r[0] = 0x80 | (r[0] & 0x3F)
+        data[i * 48:(i + 1) * 48] = r
+    return bytes(data)
+
+
+@pytest.mark.parametrize("flags", [0, 1], ids=["checked", "unchecked"])
+def test_port_matches_c_oracle_on_mixed_g1_stream(port, oracle_lib, flags):
+    n = 1500
+    data = _mixed_g1(oracle_lib, n, seed=17 + flags)
+    out, st, _, _ = oracle_run(oracle_lib, "g1_decompress", data, n, flags=flags)
+    pout, pst = port_host(port, "g1_decompress", data, flags)
+    assert sum(s != 0 for s in st) > 100  # the stream exercises the reject paths
+    assert pst == st and pout == out
+
+
+def test_port_matches_c_oracle_on_mixed_g2_stream(port, oracle_lib):
+    vecs = [bytes.fromhex(v["in"]) for v in golden("g2_decompress")]
+    rng = random.Random(23)
+    n = 400
+    data = b"".join(rng.choice(vecs) for _ in range(n))
+    out, st, _, _ = oracle_run(oracle_lib, "g2_decompress", data, n)
+    pout, pst = port_host(port, "g2_decompress", data)
+    assert pst == st and pout == out
+
+
+def test_port_matches_python_oracle_on_bn254(port):
+    """BN254 has no C restatement: the port follows kzgpot_oracle.bn254_g1_decompress_point, whose
+    golden vectors (valid, infinity, flag and range rejects, non-residues) it must reproduce."""
+    import kzgpot_oracle as O
+
+    vecs = golden("bn254_g1_decompress")
+    data = b"".join(bytes.fromhex(v["in"]) for v in vecs)
+    pout, pst = port_host(port, "bn254_g1_decompress", data)
+    for i, v in enumerate(vecs):
+        status, want = O.bn254_g1_decompress_point(bytes.fromhex(v["in"]))
+        assert pst[i] == status, v.get("note")
+        assert pout[i * 64:(i + 1) * 64] == (want if want is not None else bytes(64)), v.get("note")
+
+
+# ------------------------------------------------------------------ full populations
+@pytest.fixture(scope="module")
+def dev(gpu):
+    import torch
+
+    from kzgpot import device as D
+
+    return torch, D, torch.device("cuda", 0)
+
+
+def _product(D, torch, op, comp, rout, flags=0):
+    n = comp.numel() // OPS[op][1]
+    out = torch.empty(n * rout, dtype=torch.uint8, device=comp.device)
+    key = torch.empty(1, dtype=torch.int64, device=comp.device)
+    D.codec_dev(op, comp, out, key, flags)
+    return out, D.read_key(key)
+
+
+def test_config4_every_point_matches_the_port(port, dev):
+    """BASELINE config 4 at its size: all 2^27 G1 and 2^16 G2 records of the product codec equal
+    the oracle port's, and the port accepts every point."""
+    torch, D, cuda = dev
+    for kind, op, n, seed in (("g2", "g2_decompress", 1 << 16, 11), ("g1", "g1_decompress", 1 << 27, 10)):
+        comp, _ = D.synth(kind, seed, 0, n, cuda, with_expected=False)
+        out, key = _product(D, torch, op, comp, OPS[op][2])
+        assert key == (1 << 64) - 1
+        pout, pst = run_port(port, op, comp)
+        assert int(pst.count_nonzero()) == 0, op
+        assert torch.equal(out, pout), op
+        del comp, out, pout, pst
+        torch.cuda.empty_cache()
+
+
+def test_config3_g2_every_point_matches_the_port(port, dev):
+    torch, D, cuda = dev
+    comp, _ = D.synth("g2", 5, 0, 1 << 20, cuda, with_expected=False)
+    out, key = _product(D, torch, "g2_decompress", comp, 192)
+    pout, pst = run_port(port, "g2_decompress", comp)
+    assert key == (1 << 64) - 1 and int(pst.count_nonzero()) == 0
+    assert torch.equal(out, pout)
+
+
+def test_transcode_2e24_every_record_matches_the_port(port, dev):
+    """The uncompressed-input mode (read_g1 loop) on bench.py's 2^24 records."""
+    torch, D, cuda = dev
+    n = 1 << 24
+    _, ark = D.synth("g1", 12, 0, n, cuda)
+    pin = ark.view(n, 2, 48).flip(-1).contiguous().view(-1)  # pairing-uncompressed = byte-reversed coords
+    del ark
+    out, key = _product(D, torch, "g1_transcode", pin, 96)
+    pout, pst = run_port(port, "g1_transcode", pin)
+    assert key == (1 << 64) - 1 and int(pst.count_nonzero()) == 0
+    assert torch.equal(out, pout)
+
+
+def test_config5_every_point_matches_the_port(port, dev):
+    """BASELINE config 5 at its size: all 2^28 BN254 records (16 GiB) against the port of the
+    Python oracle's decompression."""
+    torch, D, cuda = dev
+    n = 1 << 28
+    comp, _ = D.synth("bn254", 9, 0, n, cuda, with_expected=False)
+    out, key = _product(D, torch, "bn254_g1_decompress", comp, 64)
+    assert key == (1 << 64) - 1
+    pout, pst = run_port(port, "bn254_g1_decompress", comp)
+    assert int(pst.count_nonzero()) == 0
+    assert torch.equal(out, pout)
