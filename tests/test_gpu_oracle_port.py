@@ -195,3 +195,84 @@ def test_config5_every_point_matches_the_port(port, dev):
     pout, pst = run_port(port, "bn254_g1_decompress", comp)
     assert int(pst.count_nonzero()) == 0
     assert torch.equal(out, pout)
+
+
+# ------------------------------------------------------------------ random streams at scale
+def _random_records(torch, n, rec, seed, fix):
+    """n random records of `rec` bytes on the GPU, shaped by fix(view) in place."""
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    r = torch.randint(0, 256, (n, rec), dtype=torch.uint8, device="cuda", generator=g)
+    fix(r)
+    return r.view(-1)
+
+
+def _compare_random(port, dev, op, d_in, flags=0):
+    """Product (fast subgroup test) vs the oracle port on the same random records: bytes and every
+    per-point status. Returns the port's status histogram."""
+    torch, D, _ = dev
+    _, rin, rout = OPS[op]
+    n = d_in.numel() // rin
+    out = torch.empty(n * rout, dtype=torch.uint8, device=d_in.device)
+    st = torch.empty(n, dtype=torch.uint8, device=d_in.device)
+    key = torch.empty(1, dtype=torch.int64, device=d_in.device)
+    D.codec_dev(op, d_in, out, key, flags, d_status=st)
+    pout, pst = run_port(port, op, d_in, flags)
+    assert torch.equal(st, pst), (op, (st != pst).nonzero()[:8].flatten().tolist())
+    assert torch.equal(out, pout), op
+    return {int(k): int(v) for k, v in zip(*torch.unique(pst, return_counts=True))}
+
+
+def test_random_g1_x_at_scale(port, dev):
+    """2^22 random G1 encodings (compression bit set, random infinity / greatest bits, random x):
+    about half are on the curve and, being random, outside G1 — every one of those ~2^21 points is
+    decided by the product's endomorphism test and by ark's mul_bits(r) in the port, identically."""
+    torch = dev[0]
+
+    def fix(r):
+        r[:, 0] = 0x80 | (r[:, 0] & 0x7F)
+
+    hist = _compare_random(port, dev, "g1_decompress", _random_records(torch, 1 << 22, 48, 1, fix))
+    assert hist.get(5, 0) > (1 << 19)  # NotInSubgroup: the off-subgroup on-curve points
+    assert hist.get(4, 0) > (1 << 19) and hist.get(3, 0) > 0 and hist.get(2, 0) > 0
+
+
+def test_random_g2_x_at_scale(port, dev):
+    torch = dev[0]
+
+    def fix(r):
+        r[:, 0] = 0x80 | (r[:, 0] & 0x3F)  # no infinity bit: every record reaches the square root
+        r[:, 48] &= 0x1F                      # x.c0 < 2^381: mostly < p
+
+    hist = _compare_random(port, dev, "g2_decompress", _random_records(torch, 1 << 18, 96, 2, fix))
+    assert hist.get(5, 0) > (1 << 15) and hist.get(4, 0) > (1 << 15)
+
+
+def test_random_uncompressed_at_scale(port, dev):
+    """read_g1 / read_g2 on random (x, y): almost all OFF the curve, which the reference never
+    checks — the product decides those with ark's exact double-and-add, the port with its own —
+    and SWFlags on y at random (both set: UnexpectedFlags; infinity: ark accepts any x, y)."""
+    torch = dev[0]
+
+    def fix1(r):
+        r[:, 0] &= 0x1F   # x < 2^381
+        r[:, 48] &= 0xDF  # y's top byte: random SWFlags, value bits mostly < p
+
+    def fix2(r):  # pairing G2 uncompressed: x.c1 | x.c0 | y.c1 | y.c0; the flags ride on y.c1's top byte
+        for k in (0, 48, 144):
+            r[:, k] &= 0x1F
+        r[:, 96] &= 0xDF
+
+    h1 = _compare_random(port, dev, "g1_transcode", _random_records(torch, 1 << 17, 96, 3, fix1))
+    h2 = _compare_random(port, dev, "g2_transcode", _random_records(torch, 1 << 15, 192, 4, fix2))
+    for h in (h1, h2):
+        assert h.get(6, 0) > 0 and h.get(5, 0) > 0 and h.get(0, 0) > 0, h  # flags / off-curve / infinity
+
+
+def test_random_bn254_at_scale(port, dev):
+    torch = dev[0]
+
+    def fix(r):
+        r[:, 31] &= 0xDF  # random PositiveY / Infinity flags, x mostly < p
+
+    hist = _compare_random(port, dev, "bn254_g1_decompress", _random_records(torch, 1 << 22, 32, 5, fix))
+    assert hist.get(0, 0) > (1 << 19) and hist.get(4, 0) > (1 << 19) and hist.get(6, 0) > 0
