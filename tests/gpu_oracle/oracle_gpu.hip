@@ -697,6 +697,37 @@ __device__ int bn254_decompress(uint8_t* out64, const uint8_t* enc32) {
   return ST_OK;
 }
 
+// ark-ec 0.2 GroupAffine::deserialize_unchecked into the in-memory GroupAffine (kzgpot_oracle.py:495
+// g1_deserialize_unchecked_point / :505 g2_...): coordinates < p and SWFlags only, then x, y as
+// ark-ff Montgomery limbs (6 LE u64, R = 2^384), the infinity byte and 7 bytes of padding.
+OD void put_mont(uint8_t* b, const Fq& a) {
+  for (int i = 0; i < 6; i++)
+    for (int k = 0; k < 8; k++) b[i * 8 + k] = (uint8_t)(a.l[i] >> (8 * k));
+}
+__device__ int g1_load(uint8_t* out104, const uint8_t* ark96) {
+  Fq x, y;
+  bool inf = false;
+  int st;
+  if ((st = ark_fp_read(x, ark96, false, nullptr))) return st;
+  if ((st = ark_fp_read(y, ark96 + 48, true, &inf))) return st;
+  put_mont(out104, x);
+  put_mont(out104 + 48, y);
+  out104[96] = inf ? 1 : 0;
+  for (int k = 97; k < 104; k++) out104[k] = 0;
+  return ST_OK;
+}
+__device__ int g2_load(uint8_t* out200, const uint8_t* ark192) {
+  Fq c[4];
+  bool inf = false;
+  int st;
+  for (int q = 0; q < 4; q++)
+    if ((st = ark_fp_read(c[q], ark192 + 48 * q, q == 3, q == 3 ? &inf : nullptr))) return st;
+  for (int q = 0; q < 4; q++) put_mont(out200 + 48 * q, c[q]);
+  out200[192] = inf ? 1 : 0;
+  for (int k = 193; k < 200; k++) out200[k] = 0;
+  return ST_OK;
+}
+
 // ------------------------------------------------------------------------------------ kernels
 // One lane = one point. Rejected records are zero-filled (finish, kzgpot_ref.c:655).
 __global__ void k_g1_decompress(const uint8_t* in, uint64_t n, uint8_t* out, uint8_t* status, uint32_t flags) {
@@ -748,12 +779,22 @@ __global__ void k_bn254_decompress(const uint8_t* in, uint64_t n, uint8_t* out, 
   status[i] = (uint8_t)st;
 }
 
+template <int RIN, int ROUT, int (*F)(uint8_t*, const uint8_t*)>
+__global__ void k_load(const uint8_t* in, uint64_t n, uint8_t* out, uint8_t* status) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int st = F(out + ROUT * i, in + RIN * i);
+  if (st)
+    for (int k = 0; k < ROUT; k++) out[ROUT * i + k] = 0;
+  status[i] = (uint8_t)st;
+}
+
 }  // namespace og
 
 // ------------------------------------------------------------------------------------ C entry points
 // Device pointers, asynchronous on `stream`; status gets one byte per point (0 = accepted).
 // op: 0 G1 decompress (+ check unless flags & 1), 1 G2 decompress, 2 G1 transcode, 3 G2 transcode,
-// 4 BN254 decompress. Returns 0 or a hipError_t.
+// 4 BN254 decompress, 5 G1 / 6 G2 deserialize_unchecked (the loaders). Returns 0 or a hipError_t.
 extern "C" int oracle_gpu_run(int op, const void* d_in, uint64_t n, void* d_out, void* d_status, uint32_t flags,
                               void* stream) {
   if (n == 0) return 0;
@@ -769,6 +810,8 @@ extern "C" int oracle_gpu_run(int op, const void* d_in, uint64_t n, void* d_out,
     case 2: hipLaunchKernelGGL(og::k_g1_transcode, grid, block, 0, s, in, n, out, st); break;
     case 3: hipLaunchKernelGGL(og::k_g2_transcode, grid, block, 0, s, in, n, out, st); break;
     case 4: hipLaunchKernelGGL(og::k_bn254_decompress, grid, block, 0, s, in, n, out, st); break;
+    case 5: hipLaunchKernelGGL((og::k_load<96, 104, og::g1_load>), grid, block, 0, s, in, n, out, st); break;
+    case 6: hipLaunchKernelGGL((og::k_load<192, 200, og::g2_load>), grid, block, 0, s, in, n, out, st); break;
     default: return (int)hipErrorInvalidValue;
   }
   return (int)hipGetLastError();

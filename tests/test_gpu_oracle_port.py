@@ -24,7 +24,8 @@ pytestmark = pytest.mark.gpu
 
 PORT = os.path.join(ROOT, "tests", "gpu_oracle", "build", "liboracle_gpu.so")
 OPS = {"g1_decompress": (0, 48, 96), "g2_decompress": (1, 96, 192), "g1_transcode": (2, 96, 96),
-       "g2_transcode": (3, 192, 192), "bn254_g1_decompress": (4, 32, 64)}
+       "g2_transcode": (3, 192, 192), "bn254_g1_decompress": (4, 32, 64), "g1_load": (5, 96, 104),
+       "g2_load": (6, 192, 200)}
 
 
 @pytest.fixture(scope="module")
@@ -129,6 +130,23 @@ def test_port_matches_python_oracle_on_bn254(port):
         assert pout[i * 64:(i + 1) * 64] == (want if want is not None else bytes(64)), v.get("note")
 
 
+@pytest.mark.parametrize("op,name,g2", [("g1_load", "g1_load", False), ("g2_load", "g2_load", True)])
+def test_port_matches_python_oracle_on_loader_vectors(port, op, name, g2):
+    """The loader (ark deserialize_unchecked into the in-memory GroupAffine) against the Python
+    oracle's g1/g2_deserialize_unchecked_point on the loader golden vectors."""
+    import kzgpot_oracle as O
+
+    rin, rout = (192, 200) if g2 else (96, 104)
+    fn = O.g2_deserialize_unchecked_point if g2 else O.g1_deserialize_unchecked_point
+    vecs = golden(name)
+    data = b"".join(bytes.fromhex(v["in"]) for v in vecs)
+    pout, pst = port_host(port, op, data)
+    for i, v in enumerate(vecs):
+        status, want = fn(bytes.fromhex(v["in"]))
+        assert pst[i] == status, v.get("note")
+        assert pout[i * rout:(i + 1) * rout] == (want if want is not None else bytes(rout)), v.get("note")
+
+
 # ------------------------------------------------------------------ full populations
 @pytest.fixture(scope="module")
 def dev(gpu):
@@ -182,6 +200,23 @@ def test_transcode_2e24_every_record_matches_the_port(port, dev):
     pout, pst = run_port(port, "g1_transcode", pin)
     assert key == (1 << 64) - 1 and int(pst.count_nonzero()) == 0
     assert torch.equal(out, pout)
+
+
+def test_loaders_every_record_matches_the_port(port, dev):
+    """The load_kzg_setup / load_fastkzg_setup per-point work at bench.py's sizes: 2^27 G1 ark
+    records -> 104-B GroupAffine and 2^26 G2 -> 200-B, product loader against the port."""
+    torch, D, cuda = dev
+    n = 1 << 27
+    _, ark = D.synth("g1", 13, 0, n, cuda)  # the generator's ark bytes (every record valid)
+    for op, recs, rin, rout in (("g1_load", n, 96, 104), ("g2_load", n // 2, 192, 200)):
+        src = ark[:recs * rin]
+        out, key = _product(D, torch, op, src, rout)
+        assert key == (1 << 64) - 1
+        pout, pst = run_port(port, op, src)
+        assert int(pst.count_nonzero()) == 0, op
+        assert torch.equal(out, pout), op
+        del out, pout, pst
+        torch.cuda.empty_cache()
 
 
 def test_config5_every_point_matches_the_port(port, dev):
@@ -266,6 +301,25 @@ def test_random_uncompressed_at_scale(port, dev):
     h2 = _compare_random(port, dev, "g2_transcode", _random_records(torch, 1 << 15, 192, 4, fix2))
     for h in (h1, h2):
         assert h.get(6, 0) > 0 and h.get(5, 0) > 0 and h.get(0, 0) > 0, h  # flags / off-curve / infinity
+
+
+def test_random_loader_records_at_scale(port, dev):
+    """deserialize_unchecked on random records: x / y ranges and random SWFlags on the last
+    coordinate, no curve check (most records are accepted as they are)."""
+    torch = dev[0]
+
+    def fix1(r):
+        r[:, 47] &= 0x1F  # x < 2^381 (LE: the top byte is the last)
+        r[:, 95] &= 0xDF  # y: random SWFlags
+
+    def fix2(r):
+        for k in (47, 95, 143):
+            r[:, k] &= 0x1F
+        r[:, 191] &= 0xDF
+
+    for op, rec, fix in (("g1_load", 96, fix1), ("g2_load", 192, fix2)):
+        h = _compare_random(port, dev, op, _random_records(torch, 1 << 20, rec, 6, fix))
+        assert h.get(0, 0) > 0 and h.get(3, 0) > 0 and h.get(6, 0) > 0, (op, h)
 
 
 def test_random_bn254_at_scale(port, dev):
