@@ -330,3 +330,40 @@ def test_random_bn254_at_scale(port, dev):
 
     hist = _compare_random(port, dev, "bn254_g1_decompress", _random_records(torch, 1 << 22, 32, 5, fix))
     assert hist.get(0, 0) > (1 << 19) and hist.get(4, 0) > (1 << 19) and hist.get(6, 0) > 0
+
+
+def test_preprocess_2e21_output_matches_the_port(port, dev, kzgpot_mod):
+    """The reference's own size, N = 2^21 (preprocess-kgz.rs:162-199, preprocess-fastkgz.rs:180-214):
+    a full response-layout transcript of GPU-generated points through kzgpot_preprocess_buffer, and
+    the expected kgz / fastkzg files assembled from the port's decode of every section (τG1, ατG1
+    and τG2 checked, βτG1 checked in fastkzg only, βG2 decompress-only): byte-equal files."""
+    torch, D, cuda = dev
+    n = 1 << 21
+    cnt = [("g1", 2 * n - 1), ("g2", n), ("g1", n), ("g1", n), ("g2", 1)]
+    parts = [torch.zeros(64, dtype=torch.uint8, device=cuda)]
+    for k, (kind, c) in enumerate(cnt):
+        parts.append(D.synth(kind, 90 + k, 0, c, cuda, with_expected=False)[0])
+    parts.append(torch.zeros(3 * 192 + 6 * 96, dtype=torch.uint8, device=cuda))
+    tr = torch.cat(parts)
+    del parts
+    secs, off = [], 64
+    for kind, c in cnt:
+        rin = 48 if kind == "g1" else 96
+        secs.append(tr[off:off + c * rin])
+        off += c * rin
+    host_tr = tr.cpu().numpy().tobytes()
+    for mode in (kzgpot_mod.MODE_KZG, kzgpot_mod.MODE_FASTKZG):
+        got = kzgpot_mod.preprocess_buffer(host_tr, 21, mode, n_gpus=1)
+        checked = [True, True, True, mode == kzgpot_mod.MODE_FASTKZG, False]
+        dec = []
+        for (kind, c), sec, chk in zip(cnt, secs, checked):
+            out, st = run_port(port, f"{kind}_decompress", sec, 0 if chk else 1)
+            assert int(st.count_nonzero()) == 0
+            dec.append(out)
+        tau_g1, tau_g2, alpha_g1 = dec[0], dec[1], dec[2]
+        if mode == kzgpot_mod.MODE_KZG:  # Powers + VerifierKey{g, gamma_g, h, beta_h}
+            want = torch.cat([tau_g1, alpha_g1, tau_g1[:96], alpha_g1[:96], tau_g2[:384]])
+        else:  # UniversalParams (powers_of_g, powers_of_gamma_g, h, beta_h) + powers_of_h
+            want = torch.cat([tau_g1, alpha_g1, tau_g2[:384], tau_g2])
+        assert len(got) == want.numel() == kzgpot_mod.output_size(21, mode)
+        assert got == want.cpu().numpy().tobytes(), mode
