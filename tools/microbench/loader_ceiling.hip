@@ -251,6 +251,15 @@ int main(int argc, char** argv) {
     hipLaunchKernelGGL((kzgpot::k_load<2, 256, true, 1>), dim3((unsigned)(n / 256)), dim3(512), 0, 0, in, out, n, key,
                        nullptr);
   });
+  // smaller blocks: fewer waves meet at each block barrier (32 points = one wave, 64 = two)
+  run("k_load 1c/l 32", rw, [&] {
+    hipLaunchKernelGGL((kzgpot::k_load<2, 32, true, 1>), dim3((unsigned)(n / 32)), dim3(64), 0, 0, in, out, n, key,
+                       nullptr);
+  });
+  run("k_load 1c/l 64", rw, [&] {
+    hipLaunchKernelGGL((kzgpot::k_load<2, 64, true, 1>), dim3((unsigned)(n / 64)), dim3(128), 0, 0, in, out, n, key,
+                       nullptr);
+  });
   run("k_load 2c/l 128", rw, [&] {  // one lane per point, 128 points per block
     hipLaunchKernelGGL((kzgpot::k_load<2, 128, true, 2>), dim3((unsigned)(n / 128)), dim3(128), 0, 0, in, out, n, key,
                        nullptr);
@@ -281,6 +290,14 @@ int main(int argc, char** argv) {
     });
   }
   run("k_load<G2>", (192.0 + 200.0) * n2 * 1.0, [&] { CHECK(kzgpot::launch_load(true, in, out, n2, key, nullptr, 0)); });
+  run("k_load<G2> 32", (192.0 + 200.0) * n2, [&] {
+    hipLaunchKernelGGL((kzgpot::k_load<4, 32, true, 2>), dim3((unsigned)(n2 / 32)), dim3(64), 0, 0, in, out, n2, key,
+                       nullptr);
+  });
+  run("k_load<G2> 64", (192.0 + 200.0) * n2, [&] {
+    hipLaunchKernelGGL((kzgpot::k_load<4, 64, true, 2>), dim3((unsigned)(n2 / 64)), dim3(128), 0, 0, in, out, n2, key,
+                       nullptr);
+  });
   run("k_load<G2>plain", (192.0 + 200.0) * n2, [&] {
     hipLaunchKernelGGL((kzgpot::k_load<4, 128, false>), dim3((unsigned)(n2 / 128)), dim3(256), 0, 0, in, out, n2, key,
                        nullptr);
