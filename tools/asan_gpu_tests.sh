@@ -13,7 +13,7 @@ export ASAN_OPTIONS=detect_leaks=0:abort_on_error=0:halt_on_error=1:log_path=$RO
 # everything here goes through the C ABI's host-buffer entry points, the CLI binaries aside.
 LD_PRELOAD=$ASANRT timeout -k 10 600 python -u -m pytest tests/test_gpu_preprocess.py tests/test_gpu_parity.py \
   tests/test_gpu_fuzz.py -q --timeout 300 --timeout-method thread \
-  -k "not current_device_is_restored and not load_dev_api and not bn254_synth_round_trip" \
+  -k "not current_device_is_restored and not load_dev_api and not bn254_synth_round_trip and not streamed_digest" \
   > "$ROOT/gpurun_out/asan_pytest.txt" 2>&1
 rc=$?
 ls "$ROOT"/gpurun_out/asan* >/dev/null 2>&1
