@@ -184,6 +184,28 @@ def valu_roofline(pmc, mix, kernels, points, ms, clock=None):
                       "peak = 1024 SIMDs x 2.4 GHz / avg cycles; time: this run"}
 
 
+def field_ops(census, op, points, ms):
+    """SURVEY §8d's Fp-multiply view of a codec kernel: its Montgomery reductions per point by kind
+    (the product kernels rebuilt with fp381.hpp's counting hook, tools/fpops/fp_census.hip) x this
+    run's points/s, and the fraction of the launch that those reductions would take at each
+    primitive's own microbenchmarked chip-wide peak (tools/microbench/fpops_peak.hip, 2 waves per
+    SIMD like the codecs). A fraction near 1 says the kernel's time is its reductions: the
+    additions, normalisations, selects and memory traffic are all hidden behind them."""
+    try:
+        row = next(r for r in census["rows"] if r["op"] == op and r["flags"] == 0)
+        peaks = {k: census["peaks_G_per_s"][k]["best_at_2_waves"] for k in row["per_point"]}
+    except (TypeError, KeyError, StopIteration):
+        return None
+    pps = points / (ms * 1e-3)
+    t_peak = sum(c / (peaks[k] * 1e9) for k, c in row["per_point"].items())
+    return {"reductions_per_point": row["reductions_per_point"], "by_kind": row["per_point"],
+            "reductions_per_s": row["reductions_per_point"] * pps, "peak_G_per_s": peaks,
+            "reduction_time_at_peak_ns_per_point": t_peak * 1e9, "launch_ns_per_point": 1e9 / pps,
+            "frac": t_peak * pps,
+            "source": "counts and peaks: profiles/fp_census.json (tools/fpops/census.py, peaks "
+                      + str(census.get("peaks_source")) + ", measured on another box than this run)"}
+
+
 class Sharded:
     """One point stream of n records decoded across the ranks. N > 1 with the gather: block-cyclic
     (kzgpot/dist.py) in `chunks` chunks whose in-place all-gathers overlap the next chunk's
@@ -946,6 +968,7 @@ def main():
                 "note": "integer-VALU bound, not HBM: see valu",
             },
             "valu": valu_roofline(pmc, load_json("r02_valu_mix.json"), g1_kernels, g1.m, g1_ms, clock),
+            "field_ops": field_ops(load_json("fp_census.json"), "g1_decompress", g1.m, g1_ms),
             "clock_mhz": None if clock is None else {
                 "mean": clock["mean"], "min": min(clock["per_xcd"].values()), "max": max(clock["per_xcd"].values()),
                 "xcds": len(clock["per_xcd"]),

@@ -34,7 +34,15 @@
 
 #define KZG_DEV __device__ __forceinline__
 
+// Field-operation census hook: every Montgomery reduction below names its kind. The product build
+// compiles it away; tools/fpops/fp_census.hip defines it to count the reductions per point.
+#ifndef KZG_FPOP
+#define KZG_FPOP(kind) ((void)0)
+#endif
+
 namespace kzgpot {
+
+enum class FpOp { Mul, Sqr, MulSum2, MulSum3, MulAddSqr, Mul30, Sqr30, Count };
 
 constexpr uint32_t LMASK = (1u << 28) - 1;  // BLS12-381 limbs (BlsFp::MASK)
 
@@ -69,6 +77,7 @@ KZG_DEV uint32_t dbl_u32(uint32_t x) {
 // r = a b R^-1 mod p. Requires limb-bit(a) + limb-bit(b) <= 60 (see header). Output normalized.
 template <class Tr>
 KZG_DEV void fp_mul(Fe<Tr>& r, const Fe<Tr>& a, const Fe<Tr>& b) {
+  KZG_FPOP(FpOp::Mul);
   constexpr int N = Tr::NL;
   uint32_t m[N];
   uint64_t acc = 0;
@@ -100,6 +109,7 @@ KZG_DEV void fp_mul(Fe<Tr>& r, const Fe<Tr>& a, const Fe<Tr>& b) {
 template <class Tr>
 KZG_DEV void fp_mul_sum2(Fe<Tr>& r, const Fe<Tr>& a, const Fe<Tr>& b, const Fe<Tr>& c,
                          const Fe<Tr>& d) {
+  KZG_FPOP(FpOp::MulSum2);
   constexpr int N = Tr::NL;
   uint32_t m[N];
   uint64_t acc = 0;
@@ -132,6 +142,7 @@ KZG_DEV void fp_mul_sum2(Fe<Tr>& r, const Fe<Tr>& a, const Fe<Tr>& b, const Fe<T
 template <class Tr>
 KZG_DEV void fp_mul_sum3(Fe<Tr>& r, const Fe<Tr>& a, const Fe<Tr>& b, const Fe<Tr>& c, const Fe<Tr>& d,
                          const Fe<Tr>& e, const Fe<Tr>& f) {
+  KZG_FPOP(FpOp::MulSum3);
   constexpr int N = Tr::NL;
   uint32_t m[N];
   uint64_t acc = 0;
@@ -169,6 +180,7 @@ KZG_DEV void fp_mul_sum3(Fe<Tr>& r, const Fe<Tr>& a, const Fe<Tr>& b, const Fe<T
 // whose B'^2 = 16 B^2 needs no scale: curve.hpp jac_dbl_w; bounds field_bounds_model.mul_addsqr).
 template <int S, class Tr>
 KZG_DEV void fp_mul_addsqr(Fe<Tr>& r, const Fe<Tr>& a, const Fe<Tr>& b, const Fe<Tr>& c) {
+  KZG_FPOP(FpOp::MulAddSqr);
   static_assert(S == 1 || S == 8, "scale");
   constexpr int N = Tr::NL;
   uint32_t c8[N], c16[N], m[N];  // S c and 2 S c
@@ -213,6 +225,7 @@ KZG_DEV void fp_mul_add8sqr(Fe<Tr>& r, const Fe<Tr>& a, const Fe<Tr>& b, const F
 // a's limbs must be < 2^31 so that 2 a_k fits 32 bits.
 template <class Tr>
 KZG_DEV void fp_sqr(Fe<Tr>& r, const Fe<Tr>& a) {
+  KZG_FPOP(FpOp::Sqr);
   constexpr int N = Tr::NL;
   uint32_t d[N], m[N];
 #pragma unroll
@@ -517,6 +530,7 @@ KZG_DEV int32_t sext30(uint32_t x) { return __builtin_amdgcn_sbfe((int32_t)x, 0,
 // (col * PINV30); the upper columns start their a*b partial sum at +2^29, so that the digit
 // (acc & M30) - 2^29 and the carry acc >> 30 are the balanced remainder and its exact quotient.
 KZG_DEV void f30_mul(f30& r, const f30& a, const f30& b) {
+  KZG_FPOP(FpOp::Mul30);
   constexpr int N = N30;
   int32_t m[N];
   int64_t acc = 0;
@@ -557,6 +571,7 @@ KZG_DEV int64_t mad_i64_chain(int32_t a, int32_t b, int64_t c) {
 // the compiler's re-associated sums: 94.5 against 92.6 G squarings/s (profiles/r03o_mont30_chained.txt;
 // the same chaining made the multiply 1.3 % slower, so f30_mul keeps the compiler's form).
 KZG_DEV void f30_sqr(f30& r, const f30& a) {
+  KZG_FPOP(FpOp::Sqr30);
   constexpr int N = N30;
   int32_t d[N], m[N];
 #pragma unroll

@@ -75,3 +75,29 @@ def test_fetch_probe_summary_splits_request_sizes(tmp_path):
     assert abs(row["rdreq"]["bytes_by_size_per_point"] - (786440 * 128 + 72077 * 64) / n) < 1e-3
     assert row["rdreq"]["64B"] == 72077 and row["write_B_per_point"] == 192.0
     assert row["fetch_B_per_point"] > row["rdreq"]["bytes_by_size_per_point"]  # the x2 correction's over-count
+
+
+def test_fp_census_matches_the_documented_schedule():
+    """profiles/fp_census.json (tools/fpops/census.py on the GPU) against the algorithm DESIGN §4
+    describes: one (p-3)/4 exponentiation per G1 point (376 squarings + 86 multiplies on the
+    radix-2^30 core), two per G2 point (the norm method), 2 x 62 doublings after the tripling in
+    the G1 check, each with one fused multiply-plus-square reduction; and the bench's field_ops
+    object computed from it."""
+    import importlib.util
+
+    census = json.load(open(os.path.join(ROOT, "profiles", "fp_census.json")))
+    rows = {(r["op"], r["flags"]): r for r in census["rows"]}
+    g1, g2 = rows[("g1_decompress", 0)]["per_point"], rows[("g2_decompress", 0)]["per_point"]
+    assert (g1["f30_sqr"], g1["f30_mul"]) == (376, 86)
+    assert (g2["f30_sqr"], g2["f30_mul"]) == (2 * 376, 2 * 86)
+    assert g1["fp_mul_addsqr"] == 2 * 62
+    assert rows[("g1_decompress", 1)]["per_point"].keys() >= {"f30_sqr", "f30_mul"}  # unchecked: the sqrt only
+    assert rows[("g1_decompress", 1)]["reductions_per_point"] < 0.4 * rows[("g1_decompress", 0)]["reductions_per_point"]
+    assert all(r["all_accepted"] and r["bit_exact"] for r in census["rows"])
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    fo = bench.field_ops(census, "g1_decompress", 1 << 27, 2120.0)
+    assert fo["reductions_per_point"] == sum(g1.values())
+    assert abs(fo["reductions_per_s"] - sum(g1.values()) * (1 << 27) / 2.12) < 1e3
+    assert 0.5 < fo["frac"] < 1.5
