@@ -488,7 +488,7 @@ KZG_DEV void jac_madd(jac<F>& p, Load&& load) {
 
 // [|u|] B for the affine finite base B delivered by load(x, y): |u| starts with the bits 11, so
 // the first doubling and mixed addition are one tripling from the affine base (jac_tpl_affine_w);
-// then 61 doublings, 4 mixed additions.
+// then 62 doublings (bits 61..0), 4 mixed additions.
 template <typename F, typename Load>
 KZG_DEV void mul_abs_u_affine(jac<F>& acc, Load&& load) {
   static_assert(((BLS_ABS_U >> (BLS_ABS_U_BITS - 2)) & 3) == 3, "|u| starts with the bits 11");

@@ -10,7 +10,7 @@ on subgroup points, on random curve points outside the subgroup and on small-ord
   tpl_g1 / tpl_g2         the Y-form tripling (EFD tpl-2007-bl with Z1 = 1; G2 as the triple
                           (X3 / 4, Y3 / 8, E), E = 12 x YY - MM): reference-only, the algebra the
                           device's W = 2Y forms jac_tpl_affine_w (tpl_g1_w / tpl_g2_w) scale
-  mul_abs_u_affine        [|u|] B: the tripling, then 61 doublings and 4 mixed additions
+  mul_abs_u_affine        [|u|] B: the tripling, then 62 doublings and 4 mixed additions
   in_subgroup_fast_g1     [u^2] P as [|u|] of Q1 = (X : Y : Z) run on y^2 = x^3 + 4 Z^6 from the
                           affine (X, Y), mapped back by Z' -> Z' Z; compared with phi(P) = (beta x, -y)
 """
