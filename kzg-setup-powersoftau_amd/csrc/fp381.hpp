@@ -508,7 +508,7 @@ KZG_DEV void fp_from_mont(Fe<Tr>& canon, const Fe<Tr>& a) {
 }
 
 // ------------------------------------------------------------------------------- radix-2^30 core
-// BLS12-381's square-root exponentiation (376 squarings + 85 multiplies per call: a third of the
+// BLS12-381's square-root exponentiation (382 squarings + 75 multiplies per call: a third of the
 // G1 codec's instruction stream, 40 % of the G2 codec's) runs on 13 x 30-bit BALANCED limbs:
 // int32 digits in [-2^29, 2^29), R30 = 2^390, each product one v_mad_i64_i32. Signed digits keep
 // every product below 2^58 in magnitude, so the a*b and m*p column chains (13 products each) still
@@ -647,24 +647,50 @@ KZG_DEV void fp_from_f30(fp& r, const f30& z) {
 
 // BLS12-381 r = a^((p-3)/4) on the radix-2^30 core: a (R = 2^392 Montgomery) read as an R30
 // Montgomery integer is the element 4a, so the chain computes (4a)^e and one multiply by
-// POW30_OUT = 2^392 4^-e turns it into a^e in R = 2^392 Montgomery form. Same schedule and
-// register table as the generic version below. Output canonical.
+// POW30_OUT = 2^392 4^-e turns it into a^e in R = 2^392 Montgomery form. Output canonical.
+// The register table holds the 8 odd powers BlsFp::SQRT_TABLE_EXP = a, a^3, a^7, a^9, a^11, a^13,
+// a^21, a^255, chosen for this exponent (tools/gen_constants.py, tools/sqrt_chain_search.py): the
+// windows over them take 66 multiplies where the w = 4 sliding window's a, a^3, .., a^15 took 78,
+// and building them takes 9 multiplies + 7 squarings instead of 7 + 1.
+constexpr bool bls_sqrt_table_is(const int16_t (&e)[8]) {
+  constexpr int16_t want[8] = {1, 3, 7, 9, 11, 13, 21, 255};
+  for (int k = 0; k < 8; k++)
+    if (e[k] != want[k]) return false;
+  return true;
+}
 KZG_DEV void fp_pow_pm3d4_30(fp& r, const fp& a_in) {
   typedef uint32_t v8u __attribute__((ext_vector_type(8)));
   static_assert(BlsFp::SQRT_TABLE == 8, "table held as one 8-wide register vector per limb");
+  static_assert(bls_sqrt_table_is(BlsFp::SQRT_TABLE_EXP), "the chain below builds exactly this table");
   v8u tab[N30];
-  f30 a, a2, t;
+  auto put = [&](int e, const f30& x) {
+#pragma unroll
+    for (int k = 0; k < N30; k++) tab[k][e] = (uint32_t)x.v[k];
+  };
+  f30 a, a2, a4, t, u;
   f30_from_fp(a, a_in);
-  f30_sqr(a2, a);
-  t = a;
-#pragma unroll
-  for (int k = 0; k < N30; k++) tab[k][0] = (uint32_t)a.v[k];
-#pragma clang loop unroll(full)
-  for (int e = 1; e < BlsFp::SQRT_TABLE; e++) {
-    f30_mul(t, t, a2);
-#pragma unroll
-    for (int k = 0; k < N30; k++) tab[k][e] = (uint32_t)t.v[k];
-  }
+  put(0, a);              // a
+  f30_sqr(a2, a);         // a^2
+  f30_mul(t, a, a2);      // a^3
+  put(1, t);
+  f30_sqr(a4, a2);        // a^4
+  f30_mul(t, t, a4);      // a^7
+  put(2, t);
+  f30_mul(t, t, a2);      // a^9
+  put(3, t);
+  f30_mul(t, t, a2);      // a^11
+  put(4, t);
+  f30_mul(t, t, a2);      // a^13
+  put(5, t);
+  f30_sqr(a4, a4);        // a^8
+  f30_mul(u, t, a4);      // a^21
+  put(6, u);
+  f30_mul(t, t, a2);      // a^15
+  u = t;
+#pragma unroll 1
+  for (int k = 0; k < 4; k++) f30_sqr(u, u);  // a^240
+  f30_mul(u, u, t);       // a^255
+  put(7, u);
   f30 acc;
 #pragma unroll
   for (int k = 0; k < N30; k++) acc.v[k] = (int32_t)tab[k][BlsFp::SQRT_STEP_IDX[0]];
@@ -688,20 +714,16 @@ KZG_DEV void fp_pow_pm3d4_30(fp& r, const fp& a_in) {
 
 // r = a^((p-3)/4): fixed sliding-window schedule (tools/gen_constants.py), identical for every
 // lane, so the whole wave follows one instruction stream. Loops stay rolled so one square and
-// one multiply body serve all operations (I-cache). Input limbs <= 2^30, output normalized
-// (BLS12-381: canonical, through fp_pow_pm3d4_30).
+// one multiply body serve all operations (I-cache). Input limbs <= 2^30, output normalized.
 // The 8-entry table lives in registers, one 8-wide vector per limb read with a wave-uniform
 // index (below). An earlier scratch-memory table (per-lane private memory) was cheaper in
 // instructions but its per-CU working set overflowed L2 at full occupancy: 1,479 B/point of HBM
 // re-reads, against 71 B/point with the register table (PMC FETCH_SIZE, k_g1_decompress), and
 // 2,370 -> 2,343 ms per 2^27-point G1 codec pass.
 template <class Tr>
-KZG_DEV void fp_pow_pm3d4(Fe<Tr>& r, const Fe<Tr>& a) {
-  if constexpr (__is_same(Tr, BlsFp)) {
-    fp_pow_pm3d4_30(r, a);
-    return;
-  }
+KZG_DEV void fp_pow_pm3d4_window(Fe<Tr>& r, const Fe<Tr>& a) {
   static_assert(Tr::SQRT_TABLE == 8, "table held as one 8-wide register vector per limb");
+  static_assert(Tr::SQRT_TABLE_EXP[0] == 1 && Tr::SQRT_TABLE_EXP[7] == 15, "sliding-window table a, a^3, .., a^15");
   typedef uint32_t v8u __attribute__((ext_vector_type(8)));
   // tab[k][e] = limb k of a^(2e+1): a wave-uniform (SGPR) index into a register vector becomes
   // one m0-indexed v_movrels_b32 per limb — 14 moves per lookup, no memory traffic (a scratch
@@ -733,6 +755,13 @@ KZG_DEV void fp_pow_pm3d4(Fe<Tr>& r, const Fe<Tr>& a) {
     }
   }
   r = acc;
+}
+// a^((p-3)/4) for either field: BLS12-381 on the radix-2^30 core with its own table, BN254 by
+// the sliding window above
+template <class Tr>
+KZG_DEV void fp_pow_pm3d4(Fe<Tr>& r, const Fe<Tr>& a) {
+  if constexpr (__is_same(Tr, BlsFp)) fp_pow_pm3d4_30(r, a);
+  else fp_pow_pm3d4_window(r, a);
 }
 
 // ------------------------------------------------------------------------------- reduced ops

@@ -46,7 +46,7 @@ def test_g1_fast_ladders_w_closed():
 
 def _pow_pm3d4(a):
     """fp_pow_pm3d4: table a, a^3, .., a^15 (via a^2), then squarings / table multiplies.
-    BLS12-381 runs it on the radix-2^30 core (fp_pow_pm3d4_30, proven in tests/test_fp30.py for any
+    BLS12-381 runs its own table on the radix-2^30 core (fp_pow_pm3d4_30, proven in tests/test_fp30.py for any
     input with limbs < 2^32 - 16 and value < 2^383); its output is canonical."""
     if M.NL == 14:
         assert max(a.limbs) < (1 << 32) - 16 and a.val * M.P < 2 ** 383, a

@@ -32,10 +32,11 @@ def _consts():
     pinv = int(re.search(r"PINV30 = 0x([0-9a-f]+)u", text).group(1), 16)
     steps_sq = [int(v) for v in re.search(r"SQRT_STEP_SQ\[SQRT_STEPS\] = \{([^}]*)\}", text).group(1).split(",")]
     steps_idx = [int(v) for v in re.search(r"SQRT_STEP_IDX\[SQRT_STEPS\] = \{([^}]*)\}", text).group(1).split(",")]
-    return s32["P30"], pinv, s32["POW30_OUT"], steps_sq, steps_idx
+    table = [int(v) for v in re.search(r"SQRT_TABLE_EXP\[SQRT_TABLE\] = \{([^}]*)\}", text).group(1).split(",")]
+    return s32["P30"], pinv, s32["POW30_OUT"], steps_sq, steps_idx, table
 
 
-P30, PINV30, POW30_OUT, STEP_SQ, STEP_IDX = _consts()
+P30, PINV30, POW30_OUT, STEP_SQ, STEP_IDX, TABLE_EXP = _consts()
 
 
 def val(d):
@@ -142,12 +143,25 @@ def fp_from_f30(z):
 
 
 def pow_pm3d4_30(limbs28):
+    """fp_pow_pm3d4_30 step by step: the table chain (a, a^3, a^7, a^9, a^11, a^13, a^21, a^255), the
+    header's windows over it, and the radix conversion."""
     a = f30_from_fp(limbs28)
     a2 = f30_mul(a, a, sq=True)
-    tab, t = [a], a
-    for _ in range(7):
+    t = f30_mul(a, a2)                 # a^3
+    tab = [a, t]
+    a4 = f30_mul(a2, a2, sq=True)
+    t = f30_mul(t, a4)                 # a^7
+    tab.append(t)
+    for _ in range(3):                 # a^9, a^11, a^13
         t = f30_mul(t, a2)
         tab.append(t)
+    a8 = f30_mul(a4, a4, sq=True)
+    tab.append(f30_mul(t, a8))         # a^21
+    t = f30_mul(t, a2)                 # a^15
+    u = t
+    for _ in range(4):
+        u = f30_mul(u, u, sq=True)     # a^240
+    tab.append(f30_mul(u, t))          # a^255
     acc = tab[STEP_IDX[0]]
     for nsq, idx in zip(STEP_SQ[1:], STEP_IDX[1:]):
         for _ in range(nsq):
@@ -173,6 +187,13 @@ def test_constants():
     assert val(P30) == P and all(-(1 << 29) <= d < (1 << 29) for d in P30)
     assert (PINV30 * P) % (1 << 30) == (1 << 30) - 1
     assert val(POW30_OUT) == R28 * pow(4, -E, P) % P
+    # the header's table is the one pow_pm3d4_30 (and fp_pow_pm3d4_30) builds, and its windows
+    # spell (p-3)/4
+    assert TABLE_EXP == [1, 3, 7, 9, 11, 13, 21, 255]
+    acc = TABLE_EXP[STEP_IDX[0]]
+    for nsq, idx in zip(STEP_SQ[1:], STEP_IDX[1:]):
+        acc = (acc << nsq) + (TABLE_EXP[idx] if idx >= 0 else 0)
+    assert acc == E
 
 
 def test_worst_case_columns():

@@ -10,7 +10,8 @@ with R = 2^392. Everything here is derived from p, r and u (BLS12-381) and re-ch
   * KB_c_L: c*p in a "borrowed" limb form whose limbs 0..12 are all >= 2^L - 2^(L-28), so that
     a + KB - b is a carry-free limb-wise subtraction for any b with limbs <= 2^L - 2^(L-28) and
     value < (c - 0.001) p;
-  * the sliding-window (w = 4) schedule for a^((p-3)/4) (Fp square root and inverse square root);
+  * the window schedule for a^((p-3)/4) (Fp square root and inverse square root): BLS12-381 over
+    an 8-entry table chosen for its exponent, BN254 a w = 4 sliding window;
   * 32-bit words of p for byte-level range checks; generator points (synthetic data).
 """
 from __future__ import annotations
@@ -26,7 +27,11 @@ P, R, U = O.P, O.R_ORDER, O.U_PARAM
 LB = 28                 # limb bits
 NL = 14                 # limbs (BLS12-381)
 RM = 1 << (LB * NL)     # Montgomery R = 2^392
-W = 4                   # sqrt sliding window
+W = 4                   # sqrt sliding window (BN254)
+# BLS12-381's square-root table (fp381.hpp fp_pow_pm3d4_30 builds it): 8 odd powers in registers,
+# chosen for (p-3)/4 (tools/sqrt_chain_search.py): 67 windows where the w = 4 sliding window takes
+# 79, for 6 more squarings and 2 more multiplies to build the table
+BLS_SQRT_TABLE = (1, 3, 7, 9, 11, 13, 21, 255)
 # (c, L) borrowed multiples used by the formulas in csrc/curve.hpp / fp381.hpp
 KB = [(2, 28), (4, 28), (8, 28), (8, 29), (16, 28), (32, 28), (32, 29), (64, 28), (64, 29), (64, 31), (128, 28), (128, 31),
       (4, 29), (8, 30), (16, 30), (64, 30), (16, 31)]  # the last five: the G2 ladders (curve.hpp, fp2)
@@ -130,14 +135,56 @@ def sliding_window(e, w):
     return steps
 
 
-def field_struct(name, p, nl, nw, kb, comment, lb=LB, headroom=2048):
+def table_windows(e, table, maxw=8):
+    """Fewest-multiplies window partition of e's bits over a table of odd exponents: a window starts
+    and ends on a 1 and its value is in `table`; the zeros between windows are free squarings.
+    Same step format as sliding_window, with indices into `table`."""
+    bits = bin(e)[2:]
+    n = len(bits)
+    INF = 1 << 30
+    f, pick = [0] * (n + 1), [0] * (n + 1)
+    for i in range(n - 1, -1, -1):
+        if bits[i] == "0":
+            f[i], pick[i] = f[i + 1], 0
+            continue
+        f[i] = INF
+        for w in range(1, maxw + 1):
+            if i + w <= n and bits[i + w - 1] == "1" and int(bits[i:i + w], 2) in table and 1 + f[i + w] < f[i]:
+                f[i], pick[i] = 1 + f[i + w], w
+        assert f[i] < INF, "the table cannot cover e"
+    steps, i, pending = [], 0, 0
+    while i < n:
+        if bits[i] == "0":
+            pending += 1
+            i += 1
+            continue
+        w = pick[i]
+        idx = table.index(int(bits[i:i + w], 2))
+        steps.append((0, idx) if not steps else (pending + w, idx))
+        pending, i = 0, i + w
+    if pending:
+        steps.append((pending, -1))
+    acc = None
+    for nsq, idx in steps:
+        acc = table[idx] if acc is None else (acc << nsq) + (table[idx] if idx >= 0 else 0)
+    assert acc == e, (acc, e)
+    return steps
+
+
+def field_struct(name, p, nl, nw, kb, comment, lb=LB, headroom=2048, table=None):
     """Field parameters as a traits struct consumed by the generic field core (csrc/fp381.hpp).
     lb = limb bits; headroom = the value bound (in units of p) that must fit below R."""
     rm = 1 << (lb * nl)
     assert p % 4 == 3 and p < rm // headroom
     pinv = (-pow(p, -1, 1 << lb)) % (1 << lb)
     L28 = lambda x: limbs28(x, nl, lb)  # noqa: E731
-    steps = sliding_window((p - 3) // 4, W)
+    if table is None:  # sliding window: the odd powers 1, 3, .., 2^W - 1
+        table = tuple(range(1, 2 ** W, 2))
+        steps = sliding_window((p - 3) // 4, W)
+        how = f"sliding window w={W}"
+    else:
+        steps = table_windows((p - 3) // 4, list(table))
+        how = "optimal windows over the table (tools/sqrt_chain_search.py)"
     nmul = sum(1 for st in steps if st[1] >= 0) - 1
     nsq = sum(st[0] for st in steps)
     L = [f"// {comment}: {nl} x {lb}-bit limbs, Montgomery R = 2^{lb * nl}.",
@@ -159,9 +206,10 @@ def field_struct(name, p, nl, nw, kb, comment, lb=LB, headroom=2048):
         L.append("  " + arr(nm, borrowed(c, Lb, p, nl, vmax, lb),
                             f"{c} p, limbs >= 2^{Lb} - 2^{Lb - lb}, dominates values < {vmax if vmax else c - 0.001} p"))
     L += ["  " + arr("P_WORDS", words32(p, nw), f"p as {nw} x 32-bit words (byte-level range checks)"),
-          f"  // a^((p-3)/4): sliding window w={W}, table a, a^3, .., a^{2 ** W - 1}; {nsq} squarings + {nmul} "
-          f"multiplications after the table ({2 ** (W - 1)} entries).",
-          f"  static constexpr int SQRT_TABLE = {2 ** (W - 1)};",
+          f"  // a^((p-3)/4): {how}; {nsq} squarings + {nmul} multiplications after the table of "
+          f"{len(table)} odd powers a^SQRT_TABLE_EXP[k].",
+          f"  static constexpr int SQRT_TABLE = {len(table)};",
+          "  static constexpr int16_t SQRT_TABLE_EXP[SQRT_TABLE] = {" + ", ".join(str(t) for t in table) + "};",
           f"  static constexpr int SQRT_STEPS = {len(steps)};",
           "  static constexpr int8_t SQRT_STEP_SQ[SQRT_STEPS] = {" + ", ".join(str(st[0]) for st in steps) + "};",
           "  static constexpr int8_t SQRT_STEP_IDX[SQRT_STEPS] = {" + ", ".join(str(st[1]) for st in steps) + "};",
@@ -200,7 +248,7 @@ def main():
     absu = -U
     bls_kb = [(c, Lb, None, None) for c, Lb in KB] + [(64, 31, None, "KB_EQ")]
     pow30_out = (1 << 392) * pow(4, -((P - 3) // 4), P) % P
-    fs, nsq, nmul = field_struct("BlsFp", P, NL, 12, bls_kb, "BLS12-381 Fq")
+    fs, nsq, nmul = field_struct("BlsFp", P, NL, 12, bls_kb, "BLS12-381 Fq", table=BLS_SQRT_TABLE)
     lines = [
         "// GENERATED by tools/gen_constants.py — do not edit by hand.",
         "#pragma once",
@@ -239,7 +287,7 @@ def main():
         "",
     ]
     write("bls12_381_consts.hpp", lines)
-    print(f"  BLS12-381 sqrt chain: {nsq} sq + {nmul} mul + table {2 ** (W - 1) - 1} mul + 1 sq")
+    print(f"  BLS12-381 sqrt chain: {nsq} sq + {nmul} mul after the table {BLS_SQRT_TABLE}")
 
     # BN254 (config 5): only the decompress chain runs here; fp_eq compares against normalized
     # values < 4p, which KB_8_28 dominates even with the small top limb of a 254-bit p
