@@ -467,17 +467,30 @@ int preprocess_impl(const uint8_t* tr, size_t len, uint8_t* out, int mode, uint3
     std::vector<int64_t> fb(n_shards, -1);
     std::vector<std::thread> th;
     const uint64_t per = (cnt[s] + n_shards - 1) / n_shards;
-    // With one shard the τG1 / ατG1 output (file order) is handed to the digest and writer threads
-    // chunk by chunk as it lands, so hashing and writing overlap the GPU pass instead of following it.
-    const bool stream = sink && n_shards == 1 && (s == 0 || s == 2);
-    const std::function<void(size_t, size_t)> on_chunk = [&, s, rout](size_t off, size_t m) {
-      push(dst[s] + off * rout, m * rout);
+    // The τG1 / ατG1 output (file order) is handed to the digest and writer threads chunk by chunk
+    // as it lands, so hashing and writing overlap the GPU pass instead of following it. Each shard
+    // reports its chunks in order; a record goes out once every shard before it has landed up to
+    // it (cursor), so the consumers see the file in order at any shard count.
+    const bool stream = sink && (s == 0 || s == 2);
+    std::mutex land_mu;
+    std::vector<uint64_t> landed(n_shards, 0);  // shard g: points [g per, g per + landed[g]) are in `out`
+    uint64_t cursor = 0;                         // section points [0, cursor) have been pushed
+    auto land = [&, s, rout](int g, size_t off, size_t m) {
+      std::lock_guard<std::mutex> l(land_mu);
+      landed[g] = off + m;
+      while (cursor < cnt[s]) {
+        const uint64_t h = cursor / per, avail = h * per + landed[h];
+        if (avail <= cursor) break;
+        push(dst[s] + cursor * rout, (avail - cursor) * rout);
+        cursor = avail;
+      }
     };
     for (int g = 0; g < n_shards; g++) {
       const uint64_t lo = std::min(cnt[s], g * per), hi = std::min(cnt[s], lo + per);
       th.emplace_back([&, g, lo, hi] {
         trace_thread("kzgpot.shard");
         TraceRange tr_(kSectionRange[s]);
+        const std::function<void(size_t, size_t)> on_chunk = [&, g](size_t off, size_t m) { land(g, off, m); };
         rc[g] = run_host((dev0 + g) % ndev, op, p + lo * rin, hi - lo, dst[s] ? dst[s] + lo * rout : nullptr, fl,
                          &fb[g], nullptr, stream ? &on_chunk : nullptr, dst[s] != nullptr, &in_wait);
         if (fb[g] >= 0) fb[g] += (int64_t)lo;
@@ -492,8 +505,7 @@ int preprocess_impl(const uint8_t* tr, size_t len, uint8_t* out, int mode, uint3
         if (bad_index) *bad_index = fb[g];
       }
     p += cnt[s] * rin;
-    if (!ret && sink && !stream && s == 0) push(out, off_gamma);
-    if (!ret && sink && !stream && s == 2) push(out + off_gamma, n * 96);
+    if (!ret && stream && cursor != cnt[s]) ret = KZGPOT_E_IO;  // cannot happen: every shard succeeded, so every chunk landed
   }
   uint8_t h_beta_h[2 * 192];  // kgz: τG2[0..1] for the VerifierKey (the section itself was checked)
   if (!ret && mode == KZGPOT_MODE_KZG) {

@@ -4,8 +4,8 @@ streaming file path.
 
 `n_gpus` is the shard count: shards map round-robin onto the visible devices from the current
 one, so on a one-GPU box n_gpus = 3 or 5 runs the multi-GPU host code (one thread per shard,
-per-shard first-bad offsets merged to the global minimum, output hashed and written per section
-instead of per chunk) on a single device. Expected digests and sizes are the oracle's
+per-shard first-bad offsets merged to the global minimum, output handed to the digest and writer
+in file order as far as every shard has landed) on a single device. Expected digests and sizes are the oracle's
 (tests/golden/transcript_n1024.json)."""
 import hashlib
 import json
@@ -139,14 +139,17 @@ def _synth_transcript(n_log2, seed):
 
 
 @pytest.mark.parametrize("mode", [0, 1], ids=["kgz", "fastkgz"])
-def test_streamed_digest_with_small_first_chunk(gpu, mode):
-    """N = 2^18: τG1 (2^19 - 1 points) and ατG1 run in several host chunks, and with the output
-    digest streaming from them the first chunk is the small 2^16-point one (csrc/capi.hip
-    run_host). Both digests equal hashlib's over the same bytes, τG1 / ατG1 equal the generator's;
-    then bad points in that first chunk and in a later one: the first chunk's is reported."""
-    n_log2, n = 18, 1 << 18
-    tr, expect = _synth_transcript(n_log2, seed=71 + mode)
-    res = gpu.preprocess_buffer(bytes(tr), n_log2, mode, n_gpus=1, with_digests=True)
+@pytest.mark.parametrize("n_log2,shards", [(18, 1), (19, 2)], ids=["2e18x1", "2e19x2"])
+def test_streamed_digest_with_small_first_chunk(gpu, mode, n_log2, shards):
+    """τG1 (2N - 1 points) and ατG1 run in several host chunks per shard, and with the output
+    digest streaming from them each shard's first chunk is the small 2^16-point one (csrc/capi.hip
+    run_host); with 2 shards the records reach the digest in file order only as far as both shards
+    have landed (preprocess_impl's cursor). Both digests equal hashlib's over the same bytes,
+    τG1 / ατG1 equal the generator's; then bad points in the first chunk and in a later one: the
+    first chunk's is reported."""
+    n = 1 << n_log2
+    tr, expect = _synth_transcript(n_log2, seed=71 + mode + 2 * shards)
+    res = gpu.preprocess_buffer(bytes(tr), n_log2, mode, n_gpus=shards, with_digests=True)
     g1n = (2 * n - 1) * 96
     assert res.out[:g1n] == expect["tau_g1"] and res.out[g1n:g1n + n * 96] == expect["alpha_g1"]
     assert res.transcript_digest == hashlib.blake2b(bytes(tr)).hexdigest()
@@ -154,5 +157,5 @@ def test_streamed_digest_with_small_first_chunk(gpu, mode):
     for i in ((1 << 16) - 1, 3 * (1 << 17) + 9):
         tr[64 + i * 48] &= 0x7F  # compression bit cleared: UnexpectedCompressionMode
     with pytest.raises(gpu.KzgPotError) as e:
-        gpu.preprocess_buffer(bytes(tr), n_log2, mode, n_gpus=1, with_digests=True)
+        gpu.preprocess_buffer(bytes(tr), n_log2, mode, n_gpus=shards, with_digests=True)
     assert (e.value.code, e.value.section, e.value.first_bad) == (-1, 0, (1 << 16) - 1)
