@@ -1,5 +1,7 @@
 """Field-operation census of the codec kernels, set against each primitive's measured peak.
 
+    make -C tools/fpops all      # the census library and the peak microbenchmark (CPU, ~3 min)
+    tools/microbench/bin/fpops_peak > gpurun_out/fpops_peak.txt                       # on the GPU
     python3 tools/fpops/census.py --peaks gpurun_out/fpops_peak.txt > profiles/<tag>_fp_census.json
 
 1. Runs every codec op of tools/fpops/build/libfp_census.so (the product kernels compiled with
