@@ -22,7 +22,9 @@ check), timed with HIP events on the launch stream; `valu` prices the same launc
 cycle-weighted integer-VALU issue roof (profiles/r02_valu_mix.json); `cpu_baseline` times the C
 restatement of the reference's CPU path (oracle/kzgpot_ref.c, kind "port" — the Rust reference
 cannot be built here) on a bounded sample of the same points, with the reference's schedule
-(decompression on all cores, the arkworks check on one thread). `next_rows.bn254_g1_decompress`
+(decompression on num_cpus threads as num_cpus 1.13.0 counts them, the arkworks check on one
+thread), and `cpu_baseline.e2e` times the reference's whole file-to-file pipeline in its own shape
+beside the GPU's end-to-end rows. `next_rows.bn254_g1_decompress`
 is config 5 (BN254 2^28 G1), sharded and all-gathered exactly like config 4 at N > 1.
 """
 from __future__ import annotations
@@ -78,6 +80,8 @@ def parse():
                     help="runs of 256 output records (+ the last 256) re-decoded by the C oracle")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-log2", type=int, default=15)
+    ap.add_argument("--cpu-e2e-log2", type=int, default=12,
+                    help="cpu_baseline.e2e: N of the reference-shaped CPU pipeline, file to file (0 = skip)")
     ap.add_argument("--no-next-rows", action="store_true", help="skip the SURVEY 8f rows and config 5")
     ap.add_argument("--bn254-log2", type=int, default=28, help="config 5 size (0 = skip)")
     ap.add_argument("--e2e-log2", type=int, default=21, help="end-to-end preprocess N (0 = skip)")
@@ -91,27 +95,71 @@ def oracle_lib():
     return ctypes.CDLL(path) if os.path.exists(path) else None
 
 
-def cpu_cores():
-    return min(os.cpu_count() or 1, 16)  # the GPU box grants 16 CPUs per GPU
+def affinity_cpus():
+    try:
+        return len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return os.cpu_count() or 1
+
+
+def cgroup_v1_cpu_quota():
+    """ceil(cpu.cfs_quota_us / cpu.cfs_period_us) of this process's cgroup-v1 cpu controller, or None
+    (no v1 cpu controller, or no quota) — what num_cpus 1.13.0 reads (/proc/self/cgroup +
+    /proc/self/mountinfo). It does not read cgroup v2's cpu.max."""
+    try:
+        rel = next(ln.rstrip("\n").split(":", 2)[2] for ln in open("/proc/self/cgroup")
+                   if "cpu" in ln.split(":", 2)[1].split(","))
+        for ln in open("/proc/self/mountinfo"):
+            pre, post = ln.split(" - ", 1)
+            f, opts = pre.split(), post.split()
+            if opts[0] != "cgroup" or "cpu" not in opts[2].split(","):
+                continue
+            root, mnt = f[3], f[4]
+            sub = rel[len(root):] if rel.startswith(root) else rel
+            d = os.path.join(mnt, sub.lstrip("/"))
+            quota = int(open(os.path.join(d, "cpu.cfs_quota_us")).read())
+            period = int(open(os.path.join(d, "cpu.cfs_period_us")).read())
+            return -(-quota // period) if quota > 0 and period > 0 else None
+    except (OSError, ValueError, StopIteration, IndexError):
+        pass
+    return None
+
+
+def num_cpus():
+    """The thread count the reference's `num_cpus::get()` returns on this host (num_cpus 1.13.0, the
+    version in /root/reference/Cargo.lock): min(cgroup-v1 CPU quota, affinity CPUs) when a v1 quota
+    is set, else the affinity mask's CPU count. powersoftau's decompress_all sizes its chunks by it."""
+    q = cgroup_v1_cpu_quota()
+    return min(q, affinity_cpus()) if q else affinity_cpus()
+
+
+def cgroup_v2_cpu_max():
+    """This process's cgroup-v2 cpu.max ("quota period" or "max period"), recorded beside the
+    thread counts: the CPU share the box actually grants, which num_cpus 1.13.0 does not see."""
+    try:
+        rel = next(ln.rstrip("\n").split(":", 2)[2] for ln in open("/proc/self/cgroup") if ln.startswith("0::"))
+        return open(os.path.join("/sys/fs/cgroup", rel.lstrip("/"), "cpu.max")).read().strip()
+    except (OSError, StopIteration):
+        return None
 
 
 def host_cpu():
-    """The box's CPU as SURVEY §8d asks it recorded beside the baseline: model, nproc, affinity."""
+    """The box's CPU as SURVEY §8d asks it recorded beside the baseline: model, nproc, affinity,
+    and the cgroup CPU limits."""
     model = None
     try:
         with open("/proc/cpuinfo") as f:
             model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), None)
     except OSError:
         pass
-    try:
-        affinity = len(os.sched_getaffinity(0))
-    except (AttributeError, OSError):
-        affinity = None
-    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": affinity}
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": affinity_cpus(),
+            "cgroup_v1_cpu_quota": cgroup_v1_cpu_quota(), "cgroup_v2_cpu_max": cgroup_v2_cpu_max()}
 
 
 def cpu_baseline(comp1, comp2, sample_log2):
-    """Reference-schedule CPU timing of the oracle restatement on a bounded sample."""
+    """Reference-schedule CPU timing of the oracle restatement on a bounded sample: decompression
+    on num_cpus() threads (powersoftau decompress_all, preprocess-kgz.rs:105-110), the read_g1 /
+    read_g2 subgroup check + serialize on one thread (preprocess-kgz.rs:128-160)."""
     lib = oracle_lib()
     if lib is None:
         return None
@@ -119,7 +167,7 @@ def cpu_baseline(comp1, comp2, sample_log2):
     s2 = max(1, min(s1 >> 11, comp2.numel() // 96))  # keep the workload's G1:G2 ratio (2^27 : 2^16)
     h1 = bytes(comp1[: s1 * 48].cpu().numpy())
     h2 = bytes(comp2[: s2 * 96].cpu().numpy())
-    cores = cpu_cores()
+    cores, every = num_cpus(), affinity_cpus()
     o1 = ctypes.create_string_buffer(s1 * 96)
     o2 = ctypes.create_string_buffer(s2 * 192)
     fb = ctypes.c_int64()
@@ -127,20 +175,104 @@ def cpu_baseline(comp1, comp2, sample_log2):
     r1 = lib.oracle_g1_decompress(h1, ctypes.c_size_t(s1), o1, 0, ctypes.byref(fb), None, cores, 1)
     r2 = lib.oracle_g2_decompress(h2, ctypes.c_size_t(s2), o2, 0, ctypes.byref(fb), None, cores, 1)
     dt = time.perf_counter() - t
-    # SURVEY §8d's second schedule: every stage on every core (what a parallelised reference could do)
+    # SURVEY §8d's second schedule: every stage on every CPU of the affinity mask (what a
+    # parallelised reference could do)
     t = time.perf_counter()
-    a1 = lib.oracle_g1_decompress(h1, ctypes.c_size_t(s1), o1, 0, ctypes.byref(fb), None, cores, cores)
-    a2 = lib.oracle_g2_decompress(h2, ctypes.c_size_t(s2), o2, 0, ctypes.byref(fb), None, cores, cores)
+    a1 = lib.oracle_g1_decompress(h1, ctypes.c_size_t(s1), o1, 0, ctypes.byref(fb), None, every, every)
+    a2 = lib.oracle_g2_decompress(h2, ctypes.c_size_t(s2), o2, 0, ctypes.byref(fb), None, every, every)
     dt_all = time.perf_counter() - t
     return {
         "value": (s1 + s2) / dt, "unit": "points/s", "cores": cores, "kind": "port", **host_cpu(),
+        "threads_decompress": cores, "threads_check": 1,
         "sample": f"{s1} G1 + {s2} G2 from the bench transcript, reference schedule "
-                  f"(decompress on {cores} threads, arkworks subgroup check + serialize on 1 thread); "
+                  f"(decompress on num_cpus = {cores} threads, arkworks subgroup check + serialize on 1 thread); "
                   f"{dt:.1f} s; rc={r1},{r2}",
         "seconds": dt,
-        "all_cores": {"value": (s1 + s2) / dt_all, "seconds": dt_all,
-                      "schedule": f"decompress and subgroup check both on {cores} threads; rc={a1},{a2}"},
+        "all_cores": {"value": (s1 + s2) / dt_all, "seconds": dt_all, "threads": every,
+                      "schedule": f"decompress and subgroup check both on all {every} affinity CPUs; rc={a1},{a2}"},
     }
+
+
+def e2e_transcript(n_log2, seed, dev, D, expect_names=()):
+    """A powersoftau response-layout transcript of GPU-generated valid points (as the reference's
+    `powersoftau` file: 64-B hash, τG1 2N-1, τG2 N, ατG1 N, βτG1 N, βG2 1, public key) as a host
+    numpy array, plus the generator's expected ark bytes of the sections named in expect_names."""
+    import torch
+
+    n = 1 << n_log2
+    parts, expect = [torch.zeros(64, dtype=torch.uint8, device=dev)], {}
+    for name, kind, cnt in (("tau_g1", "g1", 2 * n - 1), ("tau_g2", "g2", n), ("alpha_g1", "g1", n),
+                            ("beta_g1", "g1", n), ("beta_g2", "g2", 1)):
+        c, e = D.synth(kind, seed + len(parts), 0, cnt, dev, with_expected=name in expect_names)
+        parts.append(c)
+        if e is not None:
+            expect[name] = e.cpu().numpy()
+    parts.append(torch.zeros(3 * 192 + 6 * 96, dtype=torch.uint8, device=dev))
+    tr = torch.cat(parts).cpu().numpy()
+    return tr, expect
+
+
+def cpu_e2e(n_log2, seed, dev, D, kzgpot, gpu_rows):
+    """cpu_baseline.e2e: the reference's whole `main` in its own shape (oracle_preprocess_pipeline,
+    oracle/kzgpot_ref.c: transcript BLAKE2b check, HashReader + decompress_all on num_cpus threads,
+    the pairing-uncompressed intermediate file written and read back, read_g1 / read_g2 on one
+    thread, one unbuffered write() per coordinate; preprocess-kgz.rs:32-199,
+    preprocess-fastkgz.rs:129-213) file to file on a bounded N, per point beside the GPU's
+    preprocess_* rows (same point count per N: 2N-1 + 3N + 1). The GPU's kzgpot_preprocess_ex
+    runs on the same transcript file and its output must be byte-identical."""
+    import hashlib
+
+    import numpy as np
+    from kzgpot import _lib
+
+    lib = oracle_lib()
+    if lib is None or n_log2 <= 0:
+        return None
+    n = 1 << n_log2
+    pts = (2 * n - 1) + 3 * n + 1
+    tr, _ = e2e_transcript(n_log2, seed, dev, D)
+    tmpdir = tempfile.mkdtemp(prefix="kzgpot_cpu_e2e_")
+    src = os.path.join(tmpdir, "powersoftau")
+    tr.tofile(src)
+    digest = hashlib.blake2b(tr.tobytes()).hexdigest()
+    cores = num_cpus()
+    glib = _lib.load()
+    rows = {}
+    for mode, name in ((kzgpot.MODE_KZG, "kgz"), (kzgpot.MODE_FASTKZG, "fastkgz")):
+        unc, dst, gdst = (os.path.join(tmpdir, x) for x in ("powersoftau_uncompressed", "out", "gpu_out"))
+        stages = (ctypes.c_double * 5)()
+        t = time.perf_counter()
+        r = lib.oracle_preprocess_pipeline(src.encode(), unc.encode(), dst.encode(), ctypes.c_uint64(n), mode, cores,
+                                           digest.encode(), None, stages)
+        dt = time.perf_counter() - t
+        sec, idx = ctypes.c_int(-1), ctypes.c_int64(-1)
+        rg = glib.kzgpot_preprocess_ex(src.encode(), gdst.encode(), mode, n_log2, 1, digest.encode(), None, None,
+                                       ctypes.byref(sec), ctypes.byref(idx))
+        same = r == 0 and rg == 0 and np.array_equal(np.fromfile(dst, np.uint8), np.fromfile(gdst, np.uint8))
+        for f in (unc, dst, gdst):
+            if os.path.exists(f):
+                os.unlink(f)
+        st = list(stages)
+        # per-point cost of each stage, scaled to the reference's N = 2^21 (every stage is linear in N)
+        scale = ((2 << 21) - 1 + 3 * (1 << 21) + 1) / pts
+        gpu = gpu_rows.get(f"preprocess_{name}_e2e_file_transcript_digest") if gpu_rows else None
+        rows[name] = {
+            "n_log2": n_log2, "points": pts, "seconds": dt, "points_per_s": pts / dt, "rc": r,
+            "threads_decompress": cores, "threads_check": 1,
+            "stages_s": {"transcript_blake2b_check": st[0], "read_hash_decompress": st[1],
+                         "write_uncompressed_intermediate": st[2], "read_g1_g2_subgroup_check": st[3],
+                         "write_output_unbuffered": st[4]},
+            "extrapolated_s_at_2e21": dt * scale,
+            "output_equal_to_gpu_kzgpot_preprocess_ex": bool(same),
+            "gpu_row": None if gpu is None else {"row": f"next_rows.preprocess_{name}_e2e_file_transcript_digest",
+                                                 "points_per_s": gpu["points_per_s"],
+                                                 "speedup_per_point": gpu["points_per_s"] / (pts / dt)}}
+    os.unlink(src)
+    os.rmdir(tmpdir)
+    return {"unit": "points/s", "kind": "port", "cores": cores,
+            "sample": f"N = 2^{n_log2} synthetic response transcript ({tr.size} B) file to file per mode, the "
+                      "reference's pipeline shape (oracle_preprocess_pipeline); stage times linear in N",
+            **rows}
 
 
 def load_json(name):
@@ -510,7 +642,7 @@ def oracle_sample_check(stream, runs):
     fn = {"g1": lib.oracle_g1_decompress, "g2": lib.oracle_g2_decompress}.get(stream.kind)
     if fn is None:
         return None
-    cores, ok, pts = cpu_cores(), True, 0
+    cores, ok, pts = affinity_cpus(), True, 0
     t = time.perf_counter()
     for s in starts:
         g = stream.out[s * stream.rout:(s + 256) * stream.rout]  # gathered buffer (or the N = 1 output)
@@ -580,11 +712,14 @@ def host_api_rows(seed, dev, D, g1_log2=25, g2_log2=20):
 
 def e2e_preprocess(n_log2, seed, dev, kzgpot, D, n_gpus=1):
     """Build a synthetic response transcript (powersoftau layout, GPU-generated valid points) and
-    time the C ABI end to end in both modes: kzgpot_preprocess_buffer_ex (host buffers in and
-    out, the output buffer pre-faulted; the Python wrapper's extra copies are not the product)
-    and kzgpot_preprocess_ex (file to file, as the reference runs: the transcript streamed from
-    disk behind the GPU, the output written behind it). Checks the τG1 / ατG1 sections and both
-    digests against hashlib, and the written file against the buffer output."""
+    time the C ABI end to end: kzgpot_preprocess_buffer_ex (host buffers in and out, the output
+    buffer pre-faulted; the Python wrapper's extra copies are not the product) without digests and
+    with both, and kzgpot_preprocess_ex file to file twice — with the transcript digest only (what
+    the reference computes: download_parameters' check, preprocess-kgz.rs:32-67; it never hashes
+    its output) and with both digests. Each digest row states the single-stream BLAKE2b floor it
+    is bound by (the bytes the longest digest covers / this box's kzgpot_blake2b rate) and its
+    fraction of it. Checks the τG1 / ατG1 sections and both digests against hashlib, and the
+    written files against the buffer output."""
     import hashlib
 
     import numpy as np
@@ -592,21 +727,21 @@ def e2e_preprocess(n_log2, seed, dev, kzgpot, D, n_gpus=1):
     from kzgpot import _lib
 
     n = 1 << n_log2
-    parts, expect = [torch.zeros(64, dtype=torch.uint8, device=dev)], {}
-    for name, kind, cnt in (("tau_g1", "g1", 2 * n - 1), ("tau_g2", "g2", n), ("alpha_g1", "g1", n),
-                            ("beta_g1", "g1", n), ("beta_g2", "g2", 1)):
-        c, e = D.synth(kind, seed + len(parts), 0, cnt, dev, with_expected=name in ("tau_g1", "alpha_g1"))
-        parts.append(c)
-        if e is not None:
-            expect[name] = e.cpu().numpy()
-    parts.append(torch.zeros(3 * 192 + 6 * 96, dtype=torch.uint8, device=dev))
-    tr = torch.cat(parts).cpu().numpy()
-    del parts
+    tr, expect = e2e_transcript(n_log2, seed, dev, D, ("tau_g1", "alpha_g1"))
     assert tr.size == kzgpot.contribution_size(n_log2)
     tr_digest = hashlib.blake2b(tr.tobytes()).hexdigest()
     lib = _lib.load()
+    # the single-stream BLAKE2b rate of this box (the library's own implementation, csrc/blake2b.cpp)
+    d64 = ctypes.create_string_buffer(64)
+    lib.kzgpot_blake2b(tr.ctypes.data, ctypes.c_size_t(tr.size), d64)  # warm: pages touched, clocks up
+    t0 = time.perf_counter()
+    lib.kzgpot_blake2b(tr.ctypes.data, ctypes.c_size_t(tr.size), d64)
+    b2_gbs = tr.size / (time.perf_counter() - t0) / 1e9
     out = np.ones(max(kzgpot.output_size(n_log2, m) for m in (kzgpot.MODE_KZG, kzgpot.MODE_FASTKZG)), np.uint8)
-    rows = {}
+    devices = min(n_gpus, torch.cuda.device_count())  # shards map round-robin onto the visible devices
+    rows = {"blake2b_single_stream": {"GBs": b2_gbs, "bytes": int(tr.size),
+                                      "what": "kzgpot_blake2b over the transcript on one host thread (the floor "
+                                              "of every digest row: BLAKE2b is one sequential stream per digest)"}}
     tmpdir = tempfile.mkdtemp(prefix="kzgpot_e2e_")
     src = os.path.join(tmpdir, "powersoftau")
     tr.tofile(src)
@@ -617,22 +752,28 @@ def e2e_preprocess(n_log2, seed, dev, kzgpot, D, n_gpus=1):
         f.readinto(buf)
     read_s = time.perf_counter() - t0
     del buf
+    pts = (2 * n - 1) + 3 * n + 1
+    g1n = (2 * n - 1) * 96
+
+    def floor(nbytes, secs):
+        f = nbytes / (b2_gbs * 1e9)
+        return {"blake2b_floor_s": f, "blake2b_floor_bytes": int(nbytes), "frac_of_blake2b_floor": f / secs}
+
     for mode, name in ((kzgpot.MODE_KZG, "preprocess_kgz_e2e"), (kzgpot.MODE_FASTKZG, "preprocess_fastkgz_e2e")):
         size = kzgpot.output_size(n_log2, mode)
         sec, idx = ctypes.c_int(-1), ctypes.c_int64(-1)
+        shards = {"n_gpus": n_gpus, "shards": n_gpus, "distinct_devices": devices}
         # the GPU + PCIe part alone: the same call without the two BLAKE2b digests
         t0 = time.perf_counter()
         r0 = lib.kzgpot_preprocess_buffer_ex(tr.ctypes.data, tr.size, out.ctypes.data, mode, n_log2, n_gpus, None,
                                              None, None, ctypes.byref(sec), ctypes.byref(idx))
         dt0 = time.perf_counter() - t0
-        g1n = (2 * n - 1) * 96
         ok0 = r0 == 0 and np.array_equal(out[:g1n], expect["tau_g1"]) and \
             np.array_equal(out[g1n:g1n + n * 96], expect["alpha_g1"])
-        pts = (2 * n - 1) + 3 * n + 1
         rows[name.replace("_e2e", "_buffer_no_digest")] = {
             "workload": f"N = 2^{n_log2} response transcript -> {size} B output, host buffers, {n_gpus} shard(s) "
                         "over the visible GPUs, NO digests: decode + check + PCIe only (C ABI call timed)",
-            "seconds": dt0, "points": pts, "points_per_s": pts / dt0, "n_gpus": n_gpus,
+            "seconds": dt0, "points": pts, "points_per_s": pts / dt0, **shards,
             "sections_verified": bool(ok0)}
         out[:] = 1
         din, dout = ctypes.create_string_buffer(129), ctypes.create_string_buffer(129)
@@ -646,12 +787,29 @@ def e2e_preprocess(n_log2, seed, dev, kzgpot, D, n_gpus=1):
         ok = ok and din.value.decode() == tr_digest and dout.value.decode() == buf_digest
         rows[name] = {"workload": f"N = 2^{n_log2} response transcript ({tr.size} B) -> {size} B file, "
                                   f"host buffers, {n_gpus} shard(s), BLAKE2b of input and output (C ABI call timed)",
-                      "seconds": dt, "points": pts, "points_per_s": pts / dt, "n_gpus": n_gpus,
+                      "seconds": dt, "points": pts, "points_per_s": pts / dt, **shards,
+                      **floor(max(tr.size, size), dt), "gpu_pass_s": dt0,
                       "sections_verified": bool(ok),
                       "transcript_blake2b": din.value.decode()[:16] + "...",
                       "output_blake2b": dout.value.decode()[:16] + "..."}
-        # file to file (the reference's contract, preprocess-kgz.rs:69-126,187-194)
+        # file to file (the reference's contract, preprocess-kgz.rs:69-126,187-194), as the reference
+        # hashes: the transcript checked against its expected digest, the output not hashed
         dst = os.path.join(tmpdir, "out")
+        t0 = time.perf_counter()
+        r = lib.kzgpot_preprocess_ex(src.encode(), dst.encode(), mode, n_log2, n_gpus, tr_digest.encode(), None, None,
+                                     ctypes.byref(sec), ctypes.byref(idx))
+        dtt = time.perf_counter() - t0
+        with open(dst, "rb") as f:
+            file_digest = hashlib.blake2b(f.read()).hexdigest()
+        os.unlink(dst)
+        rows[name + "_file_transcript_digest"] = {
+            "workload": f"file to file, the reference's digest work only: kzgpot_preprocess_ex({tr.size} B transcript "
+                        "-> output file, expect_transcript_digest = its BLAKE2b; no output digest), transcript "
+                        "pread() behind the GPU, output pwrite() behind it",
+            "seconds": dtt, "points": pts, "points_per_s": pts / dtt, **shards, **floor(tr.size, dtt),
+            "gpu_pass_s": dt0, "transcript_read_s": read_s,
+            "file_verified": bool(r == 0 and file_digest == buf_digest)}
+        # file to file with both digests
         t0 = time.perf_counter()
         r = lib.kzgpot_preprocess_ex(src.encode(), dst.encode(), mode, n_log2, n_gpus, None, din, dout,
                                      ctypes.byref(sec), ctypes.byref(idx))
@@ -662,7 +820,8 @@ def e2e_preprocess(n_log2, seed, dev, kzgpot, D, n_gpus=1):
         rows[name + "_file"] = {
             "workload": f"same, file to file: kzgpot_preprocess_ex({tr.size} B transcript on local disk -> output "
                         "file), transcript pread() behind the GPU, output pwrite() behind it, both digests",
-            "seconds": dtf, "points_per_s": pts / dtf, "n_gpus": n_gpus, "buffer_path_s": dt,
+            "seconds": dtf, "points_per_s": pts / dtf, **shards, "buffer_path_s": dt,
+            **floor(max(tr.size, size), dtf), "gpu_pass_s": dt0,
             "transcript_read_s": read_s,
             "vs_buffer_plus_read": dtf / (dt + read_s),
             "file_verified": bool(r == 0 and file_digest == buf_digest == dout.value.decode())}
@@ -987,6 +1146,8 @@ def main():
                                                   D.synth("g1", args.seed, 0, 1 << args.cpu_sample_log2, dev,
                                                           with_expected=False)[0],
                                                   g2.comp, args.cpu_sample_log2)
+            if result["cpu_baseline"] is not None and args.cpu_e2e_log2 > 0:
+                result["cpu_baseline"]["e2e"] = cpu_e2e(args.cpu_e2e_log2, args.seed + 7, dev, D, kzgpot, next_rows)
         print(json.dumps(result), file=json_out, flush=True)
     if world > 1:
         # rank 0 ran the rows after the timed region (on every GPU for the e2e rows): the others

@@ -21,6 +21,7 @@
 #include <mutex>
 #include <new>
 #include <string>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -609,6 +610,39 @@ class HostBuf {
   uint8_t* base_ = nullptr;
   uint8_t* p_ = nullptr;
 };
+
+// Unmapping a file call's 1.2-1.6 GB of faulted-in pages takes ~77 ms of kernel time
+// (profiles/r04e_e2e_stages.json, after_pipeline_ms) that the caller need not wait for, so it
+// runs on a helper thread. At most one release is outstanding: the next file call joins it at
+// entry, and so does the library's unload (this object's destructor runs at exit / dlclose), so
+// back-to-back calls never stack mappings and no helper outlives the library's code. The helper
+// calls nothing but munmap (no roctx, no HIP). If no thread can be started the buffers are
+// released on the calling thread.
+class Releaser {
+ public:
+  ~Releaser() { join(); }
+  void join() {
+    std::lock_guard<std::mutex> l(mu_);
+    if (th_.joinable()) th_.join();
+  }
+  void release(std::unique_ptr<HostBuf> a, std::unique_ptr<HostBuf> b) {
+    std::lock_guard<std::mutex> l(mu_);
+    if (th_.joinable()) th_.join();
+    try {
+      th_ = std::thread([a = std::move(a), b = std::move(b)]() mutable {
+        a.reset();
+        b.reset();
+      });
+    } catch (const std::system_error&) {
+      // the callable (and the buffers it owns) was destroyed with the failed thread: released here
+    }
+  }
+
+ private:
+  std::mutex mu_;
+  std::thread th_;
+};
+Releaser g_release;
 }  // namespace
 
 extern "C" {
@@ -625,6 +659,7 @@ int kzgpot_preprocess_ex(const char* transcript_path, const char* out_path, int 
   if (bad_index) *bad_index = -1;
   if (!transcript_path || !out_path || n_log2 < 1 || n_log2 > 30) return KZGPOT_E_INVALID_ARG;
   TraceRange call_("kzgpot.preprocess_file");
+  g_release.join();  // the previous call's buffers are gone before this call maps its own
   const int fd = open(transcript_path, O_RDONLY | O_CLOEXEC);
   if (fd < 0) return KZGPOT_E_IO;
   const off_t flen = lseek(fd, 0, SEEK_END);
@@ -675,14 +710,7 @@ int kzgpot_preprocess_ex(const char* transcript_path, const char* out_path, int 
       if (!r && rename(tmp.c_str(), out_path) != 0) r = KZGPOT_E_IO;
       if (r) unlink(tmp.c_str());
     }
-    // Unmapping 1.2-1.6 GB of faulted-in pages takes ~77 ms of kernel time (profiles/r04e_e2e_stages.json,
-    // after_pipeline_ms) that the caller does not need to wait for: a detached thread releases them.
-    std::thread([t = std::move(tr), o = std::move(out)]() mutable {
-      trace_thread("kzgpot.release");
-      TraceRange rel_("kzgpot.file_release");
-      t.reset();
-      o.reset();
-    }).detach();
+    g_release.release(std::move(tr), std::move(out));  // unmapped behind the return (Releaser)
   }
   return r;
 }

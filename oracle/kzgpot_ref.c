@@ -824,3 +824,278 @@ int oracle_g1_scalar_mul_encode(const uint8_t* scalars_be32, size_t n, uint8_t* 
   }
   return 0;
 }
+
+/* ----------------------------------------------------------------- the reference pipeline, file to file */
+/* preprocess-kgz.rs / preprocess-fastkgz.rs `main` in the reference's own shape, for the CPU
+ * baseline beside the GPU end-to-end rows (bench.py cpu_baseline.e2e). Stage by stage:
+ *   0 download_parameters (preprocess-kgz.rs:32-67): read the whole transcript, BLAKE2b-512, compare;
+ *   1 powersoftau_uncompress (:69-111): a HashReader (BLAKE2b of every byte read) over an 8 KiB
+ *     BufReader; Accumulator::deserialize(Yes, No) reads each section's encodings one record at a
+ *     time, then decompress_all (powersoftau lib.rs) splits the section into chunks of
+ *     len / num_cpus points (at least 1) and runs into_affine_unchecked on one thread per chunk;
+ *   2 Accumulator::serialize(No) (:112-125): every point's pairing-uncompressed encoding through an
+ *     8 KiB BufWriter into a new `powersoftau_uncompressed` file (create_new);
+ *   3 load_powersoftau_accumulator (:128-160, fastkgz :129-178): a 1 MiB BufReader, read_g1 / read_g2
+ *     (src/lib.rs:41-80: ark deserialize_uncompressed, subgroup check mul_bits(r)) on one thread —
+ *     τG1, τG2, ατG1 (+ βτG1 for fastkgz);
+ *   4 the output (:186-194, fastkgz :190-208): File::create, then serialize_uncompressed per point
+ *     straight to the unbuffered File: one write() per Fp coordinate (2 per G1 point, 4 per G2).
+ * stage_s[0..4] receive the stage times. Returns 0, -(status) of a rejected point, -102 (I/O),
+ * -103 (size) or -104 (digest mismatch, when expect_hex is given). digest_hex (129 B, may be NULL)
+ * receives the transcript's BLAKE2b. */
+#include <fcntl.h>
+#include <stdio.h>
+#include <sys/stat.h>
+#include <time.h>
+#include <unistd.h>
+
+#include "blake2b_ref.h"
+
+static double now_s(void) {
+  struct timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return (double)t.tv_sec + 1e-9 * (double)t.tv_nsec;
+}
+
+static int write_all_fd(int fd, const uint8_t* p, size_t n) {
+  while (n) {
+    ssize_t w = write(fd, p, n);
+    if (w <= 0) return -1;
+    p += w, n -= (size_t)w;
+  }
+  return 0;
+}
+
+/* std::io::BufReader: a read at least as large as the buffer bypasses it when it is empty */
+typedef struct { int fd; uint8_t* buf; size_t cap, pos, len; oracle_blake2b_state* hash; } breader;
+static int br_read_exact(breader* r, uint8_t* dst, size_t n) {
+  uint8_t* d0 = dst;
+  size_t n0 = n;
+  while (n) {
+    if (r->pos == r->len) {
+      if (n >= r->cap) {
+        ssize_t k = read(r->fd, dst, n);
+        if (k <= 0) return -1;
+        dst += k, n -= (size_t)k;
+        continue;
+      }
+      ssize_t k = read(r->fd, r->buf, r->cap);
+      if (k <= 0) return -1;
+      r->pos = 0, r->len = (size_t)k;
+    }
+    size_t m = r->len - r->pos < n ? r->len - r->pos : n;
+    memcpy(dst, r->buf + r->pos, m);
+    r->pos += m, dst += m, n -= m;
+  }
+  if (r->hash) oracle_blake2b_update(r->hash, d0, n0); /* HashReader: every byte handed out */
+  return 0;
+}
+
+/* std::io::BufWriter */
+typedef struct { int fd; uint8_t* buf; size_t cap, len; int err; } bwriter;
+static void bw_flush(bwriter* w) {
+  if (w->len && write_all_fd(w->fd, w->buf, w->len)) w->err = 1;
+  w->len = 0;
+}
+static void bw_write_all(bwriter* w, const uint8_t* p, size_t n) {
+  if (w->len + n > w->cap) bw_flush(w);
+  if (n >= w->cap) {
+    if (write_all_fd(w->fd, p, n)) w->err = 1;
+    return;
+  }
+  memcpy(w->buf + w->len, p, n);
+  w->len += n;
+}
+
+typedef struct {
+  int g2;
+  const uint8_t* enc;
+  void* pts;
+  size_t lo, hi;
+  int64_t bad;
+  int st;
+} dchunk;
+static void* decompress_chunk(void* arg) {
+  dchunk* c = (dchunk*)arg;
+  for (size_t i = c->lo; i < c->hi; i++) {
+    int s = c->g2 ? pairing_g2_decompress(&((g2a*)c->pts)[i], c->enc + 96 * i)
+                  : pairing_g1_decompress(&((g1a*)c->pts)[i], c->enc + 48 * i);
+    if (s && c->bad < 0) c->bad = (int64_t)i, c->st = s;
+  }
+  return NULL;
+}
+/* powersoftau decompress_all: chunk_size = len / num_cpus (min 1), one scoped thread per chunk */
+static int decompress_all(int g2, const uint8_t* enc, void* pts, size_t len, int num_cpus) {
+  size_t chunk = len / (size_t)(num_cpus > 0 ? num_cpus : 1);
+  if (chunk == 0) chunk = 1;
+  size_t nt = (len + chunk - 1) / chunk;
+  dchunk* cs = (dchunk*)calloc(nt ? nt : 1, sizeof(dchunk));
+  pthread_t* tid = (pthread_t*)calloc(nt ? nt : 1, sizeof(pthread_t));
+  for (size_t t = 0; t < nt; t++) {
+    cs[t] = (dchunk){g2, enc, pts, t * chunk, (t + 1) * chunk < len ? (t + 1) * chunk : len, -1, 0};
+    if (pthread_create(&tid[t], NULL, decompress_chunk, &cs[t])) decompress_chunk(&cs[t]), tid[t] = 0;
+  }
+  int st = 0;
+  for (size_t t = 0; t < nt; t++) {
+    if (tid[t]) pthread_join(tid[t], NULL);
+    if (!st && cs[t].bad >= 0) st = cs[t].st; /* the reference keeps an arbitrary one; we keep the first */
+  }
+  free(cs);
+  free(tid);
+  return st;
+}
+
+int oracle_preprocess_pipeline(const char* transcript_path, const char* uncompressed_path, const char* out_path,
+                               uint64_t n, int fast, int num_cpus, const char* expect_hex, char* digest_hex,
+                               double* stage_s) {
+  pthread_once(&init_once, init_consts);
+  double t0 = now_s(), st_s[5] = {0, 0, 0, 0, 0};
+  const size_t len = oracle_contribution_size(n);
+  int ret = 0;
+  /* 0: download_parameters' check_file_hash on the existing file (read_to_end + BLAKE2b) */
+  {
+    int fd = open(transcript_path, O_RDONLY);
+    if (fd < 0) return -102;
+    struct stat sb;
+    if (fstat(fd, &sb) || (size_t)sb.st_size != len) {
+      close(fd);
+      return -103;
+    }
+    uint8_t* all = (uint8_t*)malloc(len);
+    size_t got = 0;
+    while (got < len) {
+      ssize_t k = read(fd, all + got, len - got);
+      if (k <= 0) break;
+      got += (size_t)k;
+    }
+    close(fd);
+    uint8_t d[64];
+    oracle_blake2b(all, got, d);
+    free(all);
+    char hex[129];
+    for (int i = 0; i < 64; i++) snprintf(hex + 2 * i, 3, "%02x", d[i]);
+    if (digest_hex) memcpy(digest_hex, hex, 129);
+    if (got != len) return -102;
+    if (expect_hex && strncmp(hex, expect_hex, 128) != 0) return -104;
+  }
+  st_s[0] = now_s() - t0;
+  const size_t cnt[5] = {2 * n - 1, n, n, n, 1};
+  const int isg2[5] = {0, 1, 0, 0, 1};
+  void* pts[5] = {0, 0, 0, 0, 0};
+  /* 1: Accumulator::deserialize(UseCompression::Yes, CheckForCorrectness::No) behind HashReader */
+  t0 = now_s();
+  {
+    int fd = open(transcript_path, O_RDONLY);
+    if (fd < 0) return -102;
+    oracle_blake2b_state h;
+    oracle_blake2b_init(&h);
+    breader r = {fd, (uint8_t*)malloc(8192), 8192, 0, 0, &h};
+    uint8_t hash64[64];
+    if (br_read_exact(&r, hash64, 64)) ret = -102;
+    for (int s = 0; s < 5 && !ret; s++) {
+      const size_t rec = isg2[s] ? 96 : 48;
+      uint8_t* enc = (uint8_t*)malloc(cnt[s] * rec);
+      for (size_t i = 0; i < cnt[s] && !ret; i++)
+        if (br_read_exact(&r, enc + rec * i, rec)) ret = -102;
+      pts[s] = calloc(cnt[s], isg2[s] ? sizeof(g2a) : sizeof(g1a));
+      if (!ret) {
+        int e = decompress_all(isg2[s], enc, pts[s], cnt[s], num_cpus);
+        if (e) ret = -e;
+      }
+      free(enc);
+    }
+    free(r.buf);
+    close(fd);
+  }
+  st_s[1] = now_s() - t0;
+  /* 2: Accumulator::serialize(UseCompression::No) through an 8 KiB BufWriter */
+  t0 = now_s();
+  if (!ret) {
+    int fd = open(uncompressed_path, O_WRONLY | O_CREAT | O_EXCL, 0644);
+    if (fd < 0) ret = -102;
+    else {
+      bwriter w = {fd, (uint8_t*)malloc(8192), 8192, 0, 0};
+      uint8_t b[192];
+      for (int s = 0; s < 5; s++)
+        for (size_t i = 0; i < cnt[s]; i++) {
+          if (isg2[s]) pairing_g2_uncompressed(b, &((g2a*)pts[s])[i]);
+          else pairing_g1_uncompressed(b, &((g1a*)pts[s])[i]);
+          bw_write_all(&w, b, isg2[s] ? 192 : 96);
+        }
+      bw_flush(&w);
+      if (w.err) ret = -102;
+      free(w.buf);
+      if (close(fd)) ret = -102;
+    }
+  }
+  for (int s = 0; s < 5; s++) free(pts[s]);
+  st_s[2] = now_s() - t0;
+  /* 3: load_powersoftau_accumulator: read_g1 / read_g2 on one thread through a 1 MiB BufReader */
+  t0 = now_s();
+  const int nload = fast ? 4 : 3; /* τG1, τG2, ατG1 (+ βτG1) */
+  void* ark[4] = {0, 0, 0, 0};
+  if (!ret) {
+    int fd = open(uncompressed_path, O_RDONLY);
+    if (fd < 0) ret = -102;
+    else {
+      breader r = {fd, (uint8_t*)malloc(1 << 20), 1 << 20, 0, 0, NULL};
+      uint8_t b[192];
+      for (int s = 0; s < nload && !ret; s++) {
+        ark[s] = calloc(cnt[s], isg2[s] ? sizeof(g2a) : sizeof(g1a));
+        for (size_t i = 0; i < cnt[s] && !ret; i++) {
+          if (br_read_exact(&r, b, isg2[s] ? 192 : 96)) {
+            ret = -102;
+            break;
+          }
+          int e = isg2[s] ? read_g2(&((g2a*)ark[s])[i], b, 1) : read_g1(&((g1a*)ark[s])[i], b, 1);
+          if (e) ret = -e; /* read_g1(f).unwrap() */
+        }
+      }
+      free(r.buf);
+      close(fd);
+    }
+  }
+  st_s[3] = now_s() - t0;
+  /* 4: serialize_uncompressed per point to the unbuffered File */
+  t0 = now_s();
+  if (!ret) {
+    int fd = open(out_path, O_WRONLY | O_CREAT | O_TRUNC, 0644);
+    if (fd < 0) ret = -102;
+    else {
+      uint8_t b[192];
+      int err = 0;
+#define W1(P)                                                               \
+  do {                                                                      \
+    ark_g1_serialize(b, (P));                                               \
+    err |= write_all_fd(fd, b, 48) | write_all_fd(fd, b + 48, 48);          \
+  } while (0)
+#define W2(P)                                                               \
+  do {                                                                      \
+    ark_g2_serialize(b, (P));                                               \
+    for (int q = 0; q < 4; q++) err |= write_all_fd(fd, b + 48 * q, 48);    \
+  } while (0)
+      g1a* tg1 = (g1a*)ark[0];
+      g2a* tg2 = (g2a*)ark[1];
+      g1a* ag1 = (g1a*)ark[2];
+      for (size_t i = 0; i < cnt[0]; i++) W1(&tg1[i]); /* powers_of_g */
+      for (size_t i = 0; i < cnt[2]; i++) W1(&ag1[i]); /* powers_of_gamma_g */
+      if (!fast) {                                    /* VerifierKey {g, gamma_g, h, beta_h} */
+        W1(&tg1[0]);
+        W1(&ag1[0]);
+        W2(&tg2[0]);
+        W2(&tg2[1]);
+      } else { /* h, beta_h, neg_powers_of_h (empty), powers_of_h */
+        W2(&tg2[0]);
+        W2(&tg2[1]);
+        for (size_t i = 0; i < cnt[1]; i++) W2(&tg2[i]);
+      }
+#undef W1
+#undef W2
+      if (close(fd) || err) ret = -102;
+    }
+  }
+  for (int s = 0; s < 4; s++) free(ark[s]);
+  st_s[4] = now_s() - t0;
+  if (stage_s) memcpy(stage_s, st_s, sizeof st_s);
+  return ret;
+}

@@ -55,6 +55,47 @@ def test_spawn_forwards_json_and_exit_code(monkeypatch, capsys):
     assert "rccl banner" in err and "torch.distributed.run" not in out
 
 
+def _alive(pid):
+    """True while pid runs: a zombie (killed but not yet reaped, e.g. when PID 1 does not reap
+    orphans) or a vanished pid counts as dead."""
+    try:
+        with open(f"/proc/{pid}/stat") as f:
+            state = f.read().rsplit(")", 1)[1].split()[0]
+    except (FileNotFoundError, ProcessLookupError, IndexError):
+        return False
+    return state not in ("Z", "X")
+
+
+def test_rank_failure_after_timed_region_fails_the_bench(capsys, tmp_path):
+    """A real torch.distributed.run with 2 ranks: rank 0 prints its JSON line and exits 0, rank 1
+    fails afterwards (as a rank could in the rows after the timed region). bench.py still forwards
+    the line, and its exit code is the launcher's non-zero one, so the driver sees the failure."""
+    b = load_bench()
+    script = ("import os, sys, time\n"
+              "r = int(os.environ['RANK'])\n"
+              "if r == 0:\n"
+              "    print('{\"metric\": \"m\", \"value\": 1}', flush=True)\n"
+              "    time.sleep(20)\n"
+              "    sys.exit(0)\n"
+              "time.sleep(1)\n"
+              "sys.exit(7)\n")
+    rank_py = tmp_path / "rank.py"
+    rank_py.write_text(script)
+    real = b.spawn_argv
+    b.spawn_argv = lambda n, port, argv: real(n, port, [])[:-1] + [str(rank_py)]
+
+    class A:
+        gpus = 2
+
+    assert b.spawn_argv(2, 1, [])[-1] == str(rank_py) and "torch.distributed.run" in b.spawn_argv(2, 1, [])
+    t = __import__("time").perf_counter()
+    rc = b.spawn_ranks(A())
+    out, _ = capsys.readouterr()
+    assert rc != 0
+    assert out.strip() == '{"metric": "m", "value": 1}'
+    assert __import__("time").perf_counter() - t < 18  # the launcher stopped rank 0 instead of waiting for it
+
+
 def test_spawned_launcher_dies_with_the_bench(tmp_path):
     """A driver timeout kills bench.py: the launcher it started must not outlive it (it would keep
     the ranks on the GPUs). The child is started with PR_SET_PDEATHSIG = SIGTERM."""
@@ -79,9 +120,7 @@ def test_spawned_launcher_dies_with_the_bench(tmp_path):
     parent.send_signal(signal.SIGKILL)  # no chance to forward anything: only the death signal helps
     parent.wait()
     for _ in range(100):
-        try:
-            os.kill(child, 0)
-        except ProcessLookupError:
+        if not _alive(child):
             break
         time.sleep(0.05)
     else:

@@ -136,6 +136,52 @@ def test_transcript_rejections(oracle_lib):
     assert r == -103
 
 
+def test_oracle_blake2b_matches_hashlib(oracle_lib):
+    """The oracle's RFC 7693 BLAKE2b-512 (oracle/blake2b_ref.c, the reference-shaped pipeline's
+    digest) equals hashlib's on lengths around the 128-B block edge and on the config-1 transcript."""
+    tr = open(os.path.join(GOLDEN, "transcript_n1024.bin"), "rb").read()
+    for m in (0, 1, 127, 128, 129, 255, 256, 257, 1000, len(tr)):
+        d = ctypes.create_string_buffer(64)
+        assert oracle_lib.oracle_blake2b(tr[:m], ctypes.c_size_t(m), d) == 0
+        assert d.raw == hashlib.blake2b(tr[:m]).digest(), m
+
+
+def _pipeline(lib, src, tmp, out, n, fast, cpus, expect=None):
+    stages = (ctypes.c_double * 5)()
+    dig = ctypes.create_string_buffer(129)
+    r = lib.oracle_preprocess_pipeline(str(src).encode(), str(tmp).encode(), str(out).encode(), ctypes.c_uint64(n),
+                                       fast, cpus, expect, dig, stages)
+    return r, dig.value.decode(), list(stages)
+
+
+def test_reference_shaped_pipeline_file_to_file(oracle_lib, tmp_path):
+    """oracle_preprocess_pipeline (bench.py's cpu_baseline.e2e): the reference's `main` in its own
+    shape — digest check, HashReader + chunked decompress, the uncompressed intermediate file,
+    single-threaded read_g1/read_g2, per-coordinate unbuffered writes — writes the same kgz /
+    fastkzg files as the in-memory restatement (digests of config 1), at any thread count."""
+    meta = json.load(open(os.path.join(GOLDEN, "transcript_n1024.json")))
+    src = os.path.join(GOLDEN, "transcript_n1024.bin")
+    for fast, key, cpus in ((0, "kgz_blake2b", 3), (1, "fastkgz_blake2b", 300)):
+        tmp, out = tmp_path / f"unc{fast}", tmp_path / f"out{fast}"
+        r, dig, stages = _pipeline(oracle_lib, src, tmp, out, 1024, fast, cpus, meta["transcript_blake2b"].encode())
+        assert r == 0 and dig == meta["transcript_blake2b"]
+        assert hashlib.blake2b(out.read_bytes()).hexdigest() == meta[key]
+        assert tmp.stat().st_size == (4 * 1024 - 1) * 96 + 1024 * 192 + 192  # pairing-uncompressed
+        assert all(s >= 0 for s in stages)
+    # create_new: an existing intermediate file is an error, as in the reference
+    r, _, _ = _pipeline(oracle_lib, src, tmp_path / "unc0", tmp_path / "x", 1024, 0, 2)
+    assert r == -102
+    # a wrong expected digest stops before anything is decoded; a bad point is reported as -(status)
+    r, _, _ = _pipeline(oracle_lib, src, tmp_path / "u2", tmp_path / "y", 1024, 0, 2, b"0" * 128)
+    assert r == -104 and not (tmp_path / "u2").exists()
+    tr = bytearray(open(src, "rb").read())
+    tr[64 + 7 * 48] &= 0x7F
+    bad = tmp_path / "bad"
+    bad.write_bytes(bytes(tr))
+    r, _, _ = _pipeline(oracle_lib, bad, tmp_path / "u3", tmp_path / "z", 1024, 0, 2)
+    assert r == -1 and not (tmp_path / "z").exists()
+
+
 @pytest.mark.parametrize("name,fn", [("g1_load", O.g1_deserialize_unchecked_point),
                                      ("g2_load", O.g2_deserialize_unchecked_point)])
 def test_python_oracle_reproduces_load_golden(name, fn):

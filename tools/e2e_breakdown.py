@@ -40,8 +40,19 @@ def main():
     for i, (kind, cnt) in enumerate((("g1", 2 * n - 1), ("g2", n), ("g1", n), ("g1", n), ("g2", 1))):
         parts.append(D.synth(kind, 100 + i, 0, cnt, dev, with_expected=False)[0])
     parts.append(torch.zeros(3 * 192 + 6 * 96, dtype=torch.uint8, device=dev))
-    tr = torch.cat(parts).cpu().numpy()
-    del parts
+    # The transcript comes to the host through a pinned buffer: the pageable `.cpu()` of round 4
+    # was the copy whose completion rocprofiler-sdk never received (profiles/r04a/r04c stage
+    # traces: "1 completion callbacks were not delivered" for correlation id 14, this process's
+    # main thread, between the generator's kernels 13 and 15 — before the first library call).
+    dt = torch.cat(parts)
+    host = torch.empty(dt.numel(), dtype=torch.uint8, pin_memory=True)
+    host.copy_(dt)
+    torch.cuda.synchronize()
+    tr = host.numpy().copy()
+    del parts, dt, host
+    import hashlib
+
+    tr_digest = hashlib.blake2b(tr.tobytes()).hexdigest()
     lib = _lib.load()
     out = np.ones(kzgpot.output_size(a.n_log2, kzgpot.MODE_FASTKZG), np.uint8)
     tmpdir = tempfile.mkdtemp(prefix="kzgpot_stages_")
@@ -53,7 +64,7 @@ def main():
     lib.kzgpot_preprocess_buffer_ex(tr.ctypes.data, tr.size, out.ctypes.data, kzgpot.MODE_FASTKZG, a.n_log2,
                                     a.shards, None, None, None, ctypes.byref(sec), ctypes.byref(idx))
     for mode, mname in ((kzgpot.MODE_KZG, "kgz"), (kzgpot.MODE_FASTKZG, "fastkgz")):
-        for kind in ("buffer_no_digest", "buffer_digests", "file_digests"):
+        for kind in ("buffer_no_digest", "buffer_digests", "file_transcript_digest", "file_digests"):
             din, dout = ctypes.create_string_buffer(129), ctypes.create_string_buffer(129)
             dig = kind != "buffer_no_digest"
             t = time.perf_counter()
@@ -61,6 +72,10 @@ def main():
                 r = lib.kzgpot_preprocess_buffer_ex(tr.ctypes.data, tr.size, out.ctypes.data, mode, a.n_log2,
                                                     a.shards, None, din if dig else None, dout if dig else None,
                                                     ctypes.byref(sec), ctypes.byref(idx))
+            elif kind == "file_transcript_digest":  # the reference's digest work: the transcript check only
+                dst = os.path.join(tmpdir, "out")
+                r = lib.kzgpot_preprocess_ex(src.encode(), dst.encode(), mode, a.n_log2, a.shards, tr_digest.encode(),
+                                             None, None, ctypes.byref(sec), ctypes.byref(idx))
             else:
                 dst = os.path.join(tmpdir, "out")
                 r = lib.kzgpot_preprocess_ex(src.encode(), dst.encode(), mode, a.n_log2, a.shards, None, din, dout,
