@@ -1053,7 +1053,7 @@ def main():
             "g2_ns_per_point": g2c * 1e6 / n3,
             "g2_valu": valu_roofline(load_json("pmc_traffic.json"), load_json("r02_valu_mix.json"),
                                      ["k_g2_decompress", "k_g2_check"] if args.split_phases else ["k_g2_codec"],
-                                     n3, g2c),
+                                     n3, g2c, clock),
             "verified_bit_exact": bool(D.read_key(k3[0:1]) == KD.NO_BAD and D.read_key(k3[1:2]) == KD.NO_BAD
                                        and torch.equal(o31, x31) and torch.equal(o32, x32))}
         # row 3, G2 (the read_g2 loop, the reference's HOT LOOP 2 for τG2): config 3's 2^20 ark G2

@@ -8,9 +8,11 @@ Per kernel (its dispatches summed):
     / SQ_ACTIVE_INST_ANY (issuing), and the share of wave cycles issuing VALU / LDS / scalar;
   * SIMD cycles per VALU instruction (GRBM_GUI_ACTIVE summed over the 8 XCDs x 128 SIMDs per XCD /
     SQ_INSTS_VALU) — the number the cycle-weighted VALU roof prices at 4.06 (G1) / 4.1 (G2);
-  * the SIMDs' VALU occupancy: SQ_ACTIVE_INST_VALU (quad-cycles, summed over waves) x 4 / the SIMD
-    cycles, i.e. the fraction of SIMD time some wave had a VALU instruction in flight;
-  * the EXEC utilisation of VALU work: SQ_THREAD_CYCLES_VALU / (64 x SQ_ACTIVE_INST_VALU x 4);
+  * the fraction of SIMD cycles the VALU spends issuing at the 4-cycle wave64 rate: 4 x SQ_INSTS_VALU /
+    the SIMD cycles (on gfx950 SQ_ACTIVE_INST_VALU counts exactly one per VALU instruction, so it
+    adds nothing to SQ_INSTS_VALU; the measured r05a ratio is 1.000 for every codec kernel);
+  * the EXEC utilisation of VALU work: SQ_THREAD_CYCLES_VALU / (64 x SQ_ACTIVE_INST_VALU) (1.0 = no
+    divergence: every VALU instruction ran all 64 lanes);
   * per wave: VALU (int32 / int64 split), SALU, SMEM, LDS, branch instructions, LDS bank conflicts.
 """
 import collections
@@ -66,8 +68,10 @@ def summarise(c):
         "active_misc_frac_of_wave_cycles": c.get("SQ_ACTIVE_INST_MISC", 0) / wc,
         "wait_inst_lds_frac": c.get("SQ_WAIT_INST_LDS", 0) / wc,
         "simd_cycles_per_valu": simd_cycles / valu if simd_cycles else None,
-        "simd_valu_occupancy": 4 * act_valu / simd_cycles if simd_cycles else None,
-        "valu_exec_utilisation": c.get("SQ_THREAD_CYCLES_VALU", 0) / (64 * 4 * act_valu) if act_valu else None,
+        "valu_issue_frac_at_4_cycles": 4 * valu / simd_cycles if simd_cycles else None,
+        "active_valu_per_valu_inst": act_valu / valu,
+        "valu_exec_utilisation": c.get("SQ_THREAD_CYCLES_VALU", 0) / (64 * act_valu) if act_valu else None,
+        "wave_quad_cycles_per_valu": wc / valu,
         "per_wave": {k: c.get(n, 0) / waves for k, n in (
             ("valu", "SQ_INSTS_VALU"), ("valu_int32", "SQ_INSTS_VALU_INT32"), ("valu_int64", "SQ_INSTS_VALU_INT64"),
             ("salu", "SQ_INSTS_SALU"), ("smem", "SQ_INSTS_SMEM"), ("lds", "SQ_INSTS_LDS"),
