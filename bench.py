@@ -102,14 +102,14 @@ def affinity_cpus():
         return os.cpu_count() or 1
 
 
-def cgroup_v1_cpu_quota():
+def cgroup_v1_cpu_quota(cgroup="/proc/self/cgroup", mountinfo="/proc/self/mountinfo"):
     """ceil(cpu.cfs_quota_us / cpu.cfs_period_us) of this process's cgroup-v1 cpu controller, or None
     (no v1 cpu controller, or no quota) — what num_cpus 1.13.0 reads (/proc/self/cgroup +
     /proc/self/mountinfo). It does not read cgroup v2's cpu.max."""
     try:
-        rel = next(ln.rstrip("\n").split(":", 2)[2] for ln in open("/proc/self/cgroup")
+        rel = next(ln.rstrip("\n").split(":", 2)[2] for ln in open(cgroup)
                    if "cpu" in ln.split(":", 2)[1].split(","))
-        for ln in open("/proc/self/mountinfo"):
+        for ln in open(mountinfo):
             pre, post = ln.split(" - ", 1)
             f, opts = pre.split(), post.split()
             if opts[0] != "cgroup" or "cpu" not in opts[2].split(","):

@@ -133,3 +133,27 @@ def test_world_size_mismatch_exits_nonzero_before_torch():
     p = subprocess.run([sys.executable, BENCH, "--gpus", "8"], env=env, capture_output=True, text=True, timeout=60)
     assert p.returncode == 2
     assert "WORLD_SIZE 1" in p.stderr and p.stdout == ""
+
+
+def test_num_cpus_follows_num_cpus_1_13(tmp_path):
+    """cpu_baseline's decompress thread count is what the reference's num_cpus::get() (1.13.0,
+    /root/reference/Cargo.lock) returns: ceil(cgroup-v1 CFS quota / period), capped by the affinity
+    CPUs, when a v1 cpu controller has a quota; otherwise the affinity count (cgroup v2's cpu.max
+    is not read by that version)."""
+    b = load_bench()
+    mnt = tmp_path / "cg" / "cpu,cpuacct"
+    d = mnt / "job"
+    d.mkdir(parents=True)
+    (d / "cpu.cfs_quota_us").write_text("150000\n")
+    (d / "cpu.cfs_period_us").write_text("100000\n")
+    cg = tmp_path / "cgroup"
+    cg.write_text("12:memory:/job\n3:cpu,cpuacct:/job\n0::/\n")
+    mi = tmp_path / "mountinfo"
+    mi.write_text(f"30 25 0:26 / {mnt} rw,nosuid - cgroup cgroup rw,cpu,cpuacct\n"
+                  f"31 25 0:27 / {tmp_path}/cg/memory rw - cgroup cgroup rw,memory\n")
+    assert b.cgroup_v1_cpu_quota(str(cg), str(mi)) == 2
+    (d / "cpu.cfs_quota_us").write_text("-1\n")  # no quota
+    assert b.cgroup_v1_cpu_quota(str(cg), str(mi)) is None
+    cg.write_text("0::/\n")  # cgroup v2 only
+    assert b.cgroup_v1_cpu_quota(str(cg), str(mi)) is None
+    assert b.num_cpus() == min(b.cgroup_v1_cpu_quota() or b.affinity_cpus(), b.affinity_cpus())

@@ -37,6 +37,19 @@ def test_test_hooks_only_in_test_build(kzgpot_mod):
     assert b"KZGPOT_RCCL_LIB" in open(_lib.TEST_LIB_PATH, "rb").read()
 
 
+def test_product_library_needs_no_profiler(kzgpot_mod):
+    """the roctx stage ranges are bound with dlopen at first use (csrc/trace.hpp), so
+    libkzgpot.so and the CLI drop-ins load on a host without rocprofiler-sdk: no DT_NEEDED entry
+    names roctx or rocprofiler, and the library still names the roctx soname it dlopens."""
+    from kzgpot import _lib
+
+    for path in (_lib.LIB_PATH, os.path.join(PKG, "build", "kzgpot-preprocess-kgz")):
+        dyn = subprocess.run(["readelf", "-d", path], capture_output=True, text=True, check=True).stdout
+        needed = [ln for ln in dyn.splitlines() if "(NEEDED)" in ln]
+        assert needed and not any("roctx" in ln or "rocprofiler" in ln for ln in needed), needed
+    assert b"librocprofiler-sdk-roctx.so.1" in open(_lib.LIB_PATH, "rb").read()
+
+
 def test_rank_failed_key_never_decodes_as_success(kzgpot_mod):
     """KZGPOT_KEY_RANK_FAILED (0), the all-reduced key when a peer could not decode its share,
     decodes to KZGPOT_E_RANK_FAILED — not to 'every point accepted' (ADVICE r03)."""
