@@ -613,11 +613,13 @@ class HostBuf {
 
 // Unmapping a file call's 1.2-1.6 GB of faulted-in pages takes ~77 ms of kernel time
 // (profiles/r04e_e2e_stages.json, after_pipeline_ms) that the caller need not wait for, so it
-// runs on a helper thread. At most one release is outstanding: the next file call joins it at
-// entry, and so does the library's unload (this object's destructor runs at exit / dlclose), so
-// back-to-back calls never stack mappings and no helper outlives the library's code. The helper
-// calls nothing but munmap (no roctx, no HIP). If no thread can be started the buffers are
-// released on the calling thread.
+// runs on a helper thread. At most one release is outstanding when a call returns: the next file
+// call joins the previous helper when it hands over its own buffers (by then, ~300 ms into its
+// pipeline, the helper has long finished — joining at entry instead cost back-to-back calls up to
+// 67 ms, profiles/r05b_e2e_stages.json), so at most two calls' buffers ever coexist, and the
+// library's unload joins the last one (this object's destructor runs at exit / dlclose), so no
+// helper outlives the library's code. The helper calls nothing but munmap (no roctx, no HIP). If
+// no thread can be started the buffers are released on the calling thread.
 class Releaser {
  public:
   ~Releaser() { join(); }
@@ -659,7 +661,6 @@ int kzgpot_preprocess_ex(const char* transcript_path, const char* out_path, int 
   if (bad_index) *bad_index = -1;
   if (!transcript_path || !out_path || n_log2 < 1 || n_log2 > 30) return KZGPOT_E_INVALID_ARG;
   TraceRange call_("kzgpot.preprocess_file");
-  g_release.join();  // the previous call's buffers are gone before this call maps its own
   const int fd = open(transcript_path, O_RDONLY | O_CLOEXEC);
   if (fd < 0) return KZGPOT_E_IO;
   const off_t flen = lseek(fd, 0, SEEK_END);

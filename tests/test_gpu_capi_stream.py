@@ -11,6 +11,7 @@ replace), :187-194 (its writer owns its buffers synchronously)."""
 import ctypes
 import hashlib
 import os
+import time
 
 import pytest
 
@@ -96,9 +97,10 @@ def _rss():
 
 def test_file_calls_back_to_back_release_buffers(capi, oracle_lib, tmp_path):
     """kzgpot_preprocess_ex unmaps its 2 x ~150 MB file buffers on a helper thread after it
-    returns, with at most one release outstanding (the next call joins it at entry). Five calls in
-    a row therefore never hold more than one call's buffers beyond the baseline, and once the last
-    release is joined (by a sixth call that fails at open) the RSS is back at the baseline."""
+    returns, with at most one release outstanding (the next call joins the previous helper when it
+    hands over its own buffers). Five calls in a row therefore never hold more than one call's
+    buffers beyond the baseline when they return, and once the last helper has run the RSS is
+    back at the baseline."""
     n_log2 = 19
     tr, tau, _ = _tiled(oracle_lib, n_log2)
     src = tmp_path / "powersoftau"
@@ -109,7 +111,8 @@ def test_file_calls_back_to_back_release_buffers(capi, oracle_lib, tmp_path):
     call = lambda path: lib.kzgpot_preprocess_ex(str(path).encode(), str(dst).encode(), 0, n_log2, 1, None, None,
                                                  None, ctypes.byref(sec), ctypes.byref(idx))
     assert call(src) == 0  # warm-up: staging buffers, HIP state
-    assert call(tmp_path / "missing") == E_IO  # joins the warm-up call's release
+    assert call(tmp_path / "missing") == E_IO  # fails at open, before any mapping
+    time.sleep(1.0)  # the warm-up call's release (~10 ms of munmap at this size) has run
     base = _rss()
     bufs = len(tr) + capi.output_size(n_log2, 0)
     peaks = []
@@ -119,5 +122,5 @@ def test_file_calls_back_to_back_release_buffers(capi, oracle_lib, tmp_path):
     assert max(peaks) < bufs + (64 << 20), peaks  # never two calls' buffers at once
     with open(dst, "rb") as f:
         assert f.read(len(tau)) == tau
-    assert call(tmp_path / "missing") == E_IO
+    time.sleep(1.0)
     assert _rss() - base < (64 << 20), (_rss() - base, peaks)
