@@ -85,6 +85,8 @@ def parse():
     ap.add_argument("--no-next-rows", action="store_true", help="skip the SURVEY 8f rows and config 5")
     ap.add_argument("--bn254-log2", type=int, default=28, help="config 5 size (0 = skip)")
     ap.add_argument("--e2e-log2", type=int, default=21, help="end-to-end preprocess N (0 = skip)")
+    ap.add_argument("--no-cli", dest="cli", action="store_false",
+                    help="skip the drop-in binaries' wall-clock rows (next_rows.cli_preprocess_*)")
     ap.add_argument("--no-host-api", dest="host_api", action="store_false",
                     help="skip the host-buffer FFI rows (next_rows.host_api)")
     return ap.parse_args()
@@ -830,6 +832,77 @@ def e2e_preprocess(n_log2, seed, dev, kzgpot, D, n_gpus=1):
     return rows
 
 
+def cli_preprocess(n_log2):
+    """The drop-in binaries as a user runs them (build/kzgpot-preprocess-{kgz,fastkgz},
+    csrc/preprocess_main.cpp, in place of `cargo run --release --bin preprocess-kgz`): process start
+    to exit, wall clock, on an N = 2^n_log2 response transcript on local disk, doing the reference's
+    digest work (the transcript's BLAKE2b-512 checked against --expect-digest; the output not
+    hashed). Runs BEFORE this process touches the GPU, so the child is never started from a process
+    holding a HIP context. The transcript tiles the config-1 transcript's valid points (host-built:
+    tools/e2e_breakdown.py); the output files' BLAKE2b is returned for the check against the
+    library's buffer call on the same transcript once the GPU is up (verify_cli)."""
+    import hashlib
+    import shutil
+    import subprocess
+
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from e2e_breakdown import tiled_transcript
+
+    tr = tiled_transcript(n_log2)
+    digest = hashlib.blake2b(tr).hexdigest()
+    tmpdir = tempfile.mkdtemp(prefix="kzgpot_cli_")
+    src = os.path.join(tmpdir, "powersoftau")
+    with open(src, "wb") as f:
+        f.write(tr)
+    rows = {"_transcript": tr}
+    try:
+        for mode in ("kgz", "fastkgz"):
+            exe = os.path.join(ROOT, "kzg-setup-powersoftau_amd", "build", f"kzgpot-preprocess-{mode}")
+            dst = os.path.join(tmpdir, "kzg_setup")
+            t0 = time.perf_counter()
+            p = subprocess.run([exe, "--n-log2", str(n_log2), "--gpus", "1", "--expect-digest", digest], cwd=tmpdir,
+                               capture_output=True, text=True, timeout=300)
+            wall = time.perf_counter() - t0
+            out_digest = None
+            if p.returncode == 0:
+                with open(dst, "rb") as f:
+                    out_digest = hashlib.blake2b(f.read()).hexdigest()
+                os.unlink(dst)
+            n = 1 << n_log2
+            pts = (2 * n - 1) + 3 * n + 1
+            rows[f"cli_preprocess_{mode}"] = {
+                "workload": f"build/kzgpot-preprocess-{mode} --n-log2 {n_log2} --gpus 1 --expect-digest <transcript "
+                            f"BLAKE2b> on a {len(tr)} B transcript file: process start to exit (HIP initialisation, "
+                            "transcript digest check, decode + check on the GPU, output file), as the reference's "
+                            "binary is run",
+                "wall_s": wall, "points": pts, "points_per_s": pts / wall, "rc": p.returncode,
+                "stdout_tail": p.stdout.strip().splitlines()[-1:] if p.stdout else None,
+                "_out_digest": out_digest}
+    finally:
+        shutil.rmtree(tmpdir, ignore_errors=True)
+    return rows
+
+
+def verify_cli(rows, n_log2, kzgpot):
+    """The CLI's files against kzgpot_preprocess_buffer_ex on the same transcript (both modes)."""
+    import hashlib
+
+    import numpy as np
+    from kzgpot import _lib
+
+    tr = np.frombuffer(rows.pop("_transcript"), np.uint8)
+    lib = _lib.load()
+    for mode, m in (("kgz", kzgpot.MODE_KZG), ("fastkgz", kzgpot.MODE_FASTKZG)):
+        row = rows[f"cli_preprocess_{mode}"]
+        out = np.empty(kzgpot.output_size(n_log2, m), np.uint8)
+        sec, idx = ctypes.c_int(-1), ctypes.c_int64(-1)
+        r = lib.kzgpot_preprocess_buffer_ex(tr.ctypes.data, tr.size, out.ctypes.data, m, n_log2, 1, None, None, None,
+                                            ctypes.byref(sec), ctypes.byref(idx))
+        row["file_equal_to_library_buffer_call"] = bool(r == 0 and row.pop("_out_digest") ==
+                                                        hashlib.blake2b(out).hexdigest())
+    return rows
+
+
 def spawn_ranks(args) -> int:
     """`bench.py --gpus N` (N > 1) with no launcher around it: run `torch.distributed.run
     --nproc-per-node N ... bench.py <same args>` as a child process (never exec: this process has
@@ -917,6 +990,10 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # the drop-in binaries, timed as child processes before this process touches the GPU
+    cli_rows = None
+    if world == 1 and not args.no_next_rows and args.e2e_log2 > 0 and args.cli:
+        cli_rows = cli_preprocess(args.e2e_log2)
 
     import torch
     import torch.distributed as dist
@@ -1078,6 +1155,8 @@ def main():
         # ranks wait on the host
         if args.e2e_log2 > 0:
             next_rows.update(e2e_preprocess(args.e2e_log2, args.seed + 3, dev, kzgpot, D, n_gpus=world))
+        if cli_rows is not None:
+            next_rows.update(verify_cli(cli_rows, args.e2e_log2, kzgpot))
 
     ms_per_step = elapsed * 1e3 / args.steps
     value = (n1 + n2) * args.steps / elapsed

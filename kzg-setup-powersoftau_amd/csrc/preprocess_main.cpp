@@ -10,7 +10,9 @@
 //  * no powersoftau_uncompressed intermediate (preprocess-kgz.rs:69-127): the GPU decodes the
 //    compressed transcript straight into the arkworks file.
 // Extra options (for other transcript sizes and synthetic transcripts): --transcript, --out,
-// --n-log2, --gpus, --no-digest-check.
+// --n-log2, --gpus, --expect-digest, --no-digest-check, --output-digest. By default the work is the
+// reference's: the transcript's BLAKE2b-512 is checked and the output is not hashed (the reference
+// never hashes it; --output-digest adds that second stream and prints it).
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -37,12 +39,15 @@ constexpr int kPanicExit = 101;  // what a panicking Rust binary exits with
 }
 
 void usage(const char* prog) {
-  printf("usage: %s [--transcript PATH] [--out PATH] [--n-log2 N] [--gpus N] [--no-digest-check]\n"
+  printf("usage: %s [--transcript PATH] [--out PATH] [--n-log2 N] [--gpus N] [--expect-digest HEX]\n"
+         "          [--no-digest-check] [--output-digest]\n"
          "  --transcript PATH   powersoftau response file (default: ./powersoftau, as the reference)\n"
          "  --out PATH          output file (default: ./kzg_setup, KZG_SETUP_FILE in src/lib.rs:20)\n"
          "  --n-log2 N          2^N tau powers (default 21, TAU_POWERS_LENGTH)\n"
          "  --gpus N            GPUs to use (default 0 = every visible one)\n"
-         "  --no-digest-check   skip the POWERSOFTAU_DIGEST check (transcripts other than the ceremony's)\n",
+         "  --expect-digest HEX the transcript's expected BLAKE2b-512 (default: POWERSOFTAU_DIGEST)\n"
+         "  --no-digest-check   skip the transcript digest check (transcripts other than the ceremony's)\n"
+         "  --output-digest     also compute and print the output file's BLAKE2b-512\n",
          prog);
 }
 
@@ -54,14 +59,17 @@ int main(int argc, char** argv) {
   const char* out = "kzg_setup";
   unsigned n_log2 = 21;
   int gpus = 0;
-  bool check_digest = true;
+  bool check_digest = true, output_digest = false;
+  const char* expect = kPowersoftauDigest;
   for (int i = 1; i < argc; i++) {
     const bool has_val = i + 1 < argc;
     if (!strcmp(argv[i], "--transcript") && has_val) transcript = argv[++i];
     else if (!strcmp(argv[i], "--out") && has_val) out = argv[++i];
     else if (!strcmp(argv[i], "--n-log2") && has_val) n_log2 = (unsigned)atoi(argv[++i]);
     else if (!strcmp(argv[i], "--gpus") && has_val) gpus = atoi(argv[++i]);
+    else if (!strcmp(argv[i], "--expect-digest") && has_val) expect = argv[++i];
     else if (!strcmp(argv[i], "--no-digest-check")) check_digest = false;
+    else if (!strcmp(argv[i], "--output-digest")) output_digest = true;
     else if (!strcmp(argv[i], "-h") || !strcmp(argv[i], "--help")) {
       usage(argv[0]);
       return 0;
@@ -71,6 +79,7 @@ int main(int argc, char** argv) {
     }
   }
   if (n_log2 < 1 || n_log2 > 28) panic_exit("--n-log2 must be in 1..28");
+  if (strlen(expect) != 128) panic_exit("--expect-digest must be 128 hex characters");
 
   // download_parameters (preprocess-kgz.rs:32-67): only the "existing file" branch exists here
   struct stat sb;
@@ -96,14 +105,14 @@ int main(int argc, char** argv) {
   char tdig[129] = {0}, odig[129] = {0};
   int bad_section = -1;
   int64_t bad_index = -1;
-  const int rc = kzgpot_preprocess_ex(transcript, out, KZGPOT_CLI_MODE, n_log2, gpus,
-                                      check_digest ? kPowersoftauDigest : nullptr, tdig, odig, &bad_section, &bad_index);
+  const int rc = kzgpot_preprocess_ex(transcript, out, KZGPOT_CLI_MODE, n_log2, gpus, check_digest ? expect : nullptr,
+                                      tdig, output_digest ? odig : nullptr, &bad_section, &bad_index);
   if (rc == KZGPOT_E_DIGEST) {
     char msg[512];
     snprintf(msg, sizeof msg,
              "called `Result::unwrap()` on an `Err` value: failed validation (expected: %s, got %s); this build does "
              "not download a replacement",
-             kPowersoftauDigest, tdig);
+             expect, tdig);
     panic_exit(msg);
   }
   if (rc > -100 && rc < 0) {  // a rejected point: the reference's unwrap() / expect() panics
@@ -121,7 +130,7 @@ int main(int argc, char** argv) {
   if (check_digest) printf("Checking passed, using existing %s file.\n", transcript);
   printf("Loaded Powers of Tau\n");
   printf("transcript BLAKE2b-512: %s\n", tdig);
-  printf("output BLAKE2b-512: %s\n", odig);
+  if (output_digest) printf("output BLAKE2b-512: %s\n", odig);
   printf("Done serializing. KZG parameters are stored in %s\n", out);
   return 0;
 }

@@ -24,8 +24,8 @@ def test_cli_preprocess_config1(mode, tmp_path):
     meta = json.load(open(os.path.join(GOLDEN, "transcript_n1024.json")))
     shutil.copy(os.path.join(GOLDEN, "transcript_n1024.bin"), tmp_path / "powersoftau")
     exe = os.path.join(PKG, "build", f"kzgpot-preprocess-{mode}")
-    r = subprocess.run([exe, "--n-log2", "10", "--no-digest-check"], cwd=tmp_path, capture_output=True, text=True,
-                       timeout=120)
+    r = subprocess.run([exe, "--n-log2", "10", "--no-digest-check", "--output-digest"], cwd=tmp_path,
+                       capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     out = (tmp_path / "kzg_setup").read_bytes()
     assert len(out) == meta[f"{mode}_size"]
@@ -33,6 +33,16 @@ def test_cli_preprocess_config1(mode, tmp_path):
     assert f"output BLAKE2b-512: {meta[f'{mode}_blake2b']}" in r.stdout
     assert f"transcript BLAKE2b-512: {meta['transcript_blake2b']}" in r.stdout
     (tmp_path / "kzg_setup").unlink()
+    # the reference's own work: the transcript checked against a given digest, the output not hashed
+    r = subprocess.run([exe, "--n-log2", "10", "--expect-digest", meta["transcript_blake2b"]], cwd=tmp_path,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert "output BLAKE2b-512" not in r.stdout and "Checking passed" in r.stdout
+    assert hashlib.blake2b((tmp_path / "kzg_setup").read_bytes()).hexdigest() == meta[f"{mode}_blake2b"]
+    (tmp_path / "kzg_setup").unlink()
+    r = subprocess.run([exe, "--n-log2", "10", "--expect-digest", "0" * 128], cwd=tmp_path, capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 101 and "failed validation" in r.stderr and not (tmp_path / "kzg_setup").exists()
     r = subprocess.run([exe, "--n-log2", "10"], cwd=tmp_path, capture_output=True, text=True, timeout=120)
     assert r.returncode == 101 and "failed validation" in r.stderr
     assert not (tmp_path / "kzg_setup").exists()

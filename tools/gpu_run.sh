@@ -7,6 +7,7 @@
 # gpurun_out/TAG_<step>.* ; the first failing step ends the run with exit code 10 + its position
 # (nothing more touches the GPU after a failure, a fault or a time limit). Steps:
 #   pytest        the whole GPU suite (pytest -m gpu)
+#   quicktests    the CLI, C-ABI stream and preprocess GPU tests only
 #   smoke         __graft_entry__.smoke()
 #   bench         python bench.py (the default line: config 4 + every row + cpu_baseline)
 #   bench_quick   bench.py without the CPU baseline and the e2e rows (kernel numbers only)
@@ -35,6 +36,8 @@ for step in "$@"; do
   case $step in
     pytest) timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread \
               --durations=15 > ${o}_pytest_gpu.txt 2>&1 ;;
+    quicktests) timeout -k 10 600 python -u -m pytest tests/test_cli_gpu.py tests/test_gpu_capi_stream.py \
+                  tests/test_gpu_preprocess.py -x -v --timeout 300 --timeout-method thread > ${o}_quicktests.txt 2>&1 ;;
     smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > ${o}_smoke.txt 2>&1 ;;
     bench) timeout -k 10 600 python -u bench.py > ${o}_bench_n1.json 2> ${o}_bench.err ;;
     bench_quick) timeout -k 10 400 python -u bench.py --no-cpu-baseline --e2e-log2 0 --no-host-api \
