@@ -14,6 +14,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <condition_variable>
 #include <deque>
 #include <functional>
@@ -393,19 +394,14 @@ int preprocess_impl(const uint8_t* tr, size_t len, uint8_t* out, int mode, uint3
     return KZGPOT_E_INVALID_ARG;
   if (expect_in_hex && strlen(expect_in_hex) != 128) return KZGPOT_E_INVALID_ARG;
   if (len != kzgpot_contribution_size(n_log2)) return KZGPOT_E_SIZE;
-  const int ndev = device_count();
-  if (ndev <= 0) return KZGPOT_E_DEVICE;
-  if (n_shards <= 0) n_shards = ndev;
-  n_shards = std::min(n_shards, 64);
-  int dev0 = current_device();
-  if (dev0 < 0 || dev0 >= ndev) dev0 = 0;
-  const uint64_t n = 1ull << n_log2;
-  const InputWait in_wait{io.in_wm, tr};
 
   // transcript digest (download_parameters' check, preprocess-kgz.rs:51-61) beside the GPU pass;
-  // a transcript still streaming from disk is hashed as it arrives
+  // a transcript still streaming from disk is hashed as it arrives. It is the call's critical path
+  // (one sequential BLAKE2b stream), so it starts before anything touches HIP: in a fresh process
+  // (the CLI drop-ins) the runtime's initialisation then overlaps it instead of preceding it.
   uint8_t in_digest[64];
   bool in_ok = true;
+  std::atomic<bool> abandon{false};  // set when the call fails before the GPU pass starts
   std::thread in_hash;
   const bool want_in = expect_in_hex || in_hex;
   TraceRange call_("kzgpot.preprocess");
@@ -413,11 +409,10 @@ int preprocess_impl(const uint8_t* tr, size_t len, uint8_t* out, int mode, uint3
     in_hash = std::thread([&] {
       trace_thread("kzgpot.blake2b.transcript");
       TraceRange tr_("kzgpot.blake2b.transcript");
-      if (!io.in_wm) return blake2b_512(tr, len, in_digest);
       Blake2b h;
       for (size_t off = 0; off < len;) {
         const size_t m = std::min<size_t>(len - off, (size_t)32 << 20);
-        if (!io.in_wm->wait(off + m)) {
+        if (abandon.load(std::memory_order_relaxed) || (io.in_wm && !io.in_wm->wait(off + m))) {
           in_ok = false;
           return;
         }
@@ -426,6 +421,18 @@ int preprocess_impl(const uint8_t* tr, size_t len, uint8_t* out, int mode, uint3
       }
       h.finalize(in_digest);
     });
+  const int ndev = device_count();
+  if (ndev <= 0) {
+    abandon = true;
+    if (in_hash.joinable()) in_hash.join();
+    return KZGPOT_E_DEVICE;
+  }
+  if (n_shards <= 0) n_shards = ndev;
+  n_shards = std::min(n_shards, 64);
+  int dev0 = current_device();
+  if (dev0 < 0 || dev0 >= ndev) dev0 = 0;
+  const uint64_t n = 1ull << n_log2;
+  const InputWait in_wait{io.in_wm, tr};
   // output consumers, fed the file's byte ranges in file order
   Blake2b out_h;
   std::unique_ptr<OrderedWorker> out_hash, out_write;
