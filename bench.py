@@ -860,9 +860,17 @@ def cli_preprocess(n_log2):
             exe = os.path.join(ROOT, "kzg-setup-powersoftau_amd", "build", f"kzgpot-preprocess-{mode}")
             dst = os.path.join(tmpdir, "kzg_setup")
             t0 = time.perf_counter()
-            p = subprocess.run([exe, "--n-log2", str(n_log2), "--gpus", "1", "--expect-digest", digest], cwd=tmpdir,
-                               capture_output=True, text=True, timeout=300)
+            p = subprocess.run([exe, "--n-log2", str(n_log2), "--gpus", "1", "--expect-digest", digest, "--timing"],
+                               cwd=tmpdir, capture_output=True, text=True, timeout=300)
             wall = time.perf_counter() - t0
+            phases = None
+            for ln in (p.stdout or "").splitlines():
+                if ln.startswith("timing: main "):  # "timing: main A s after process start, library call done B s after"
+                    w = ln.split()
+                    main_s, done_s = float(w[2]), float(w[10])
+                    phases = {"process_start_to_main_s": main_s, "library_call_s": done_s - main_s,
+                              "after_call_to_exit_s": wall - done_s,
+                              "note": "start and main from /proc/self/stat (10 ms ticks); exit = wall - call done"}
             out_digest = None
             if p.returncode == 0:
                 with open(dst, "rb") as f:
@@ -875,7 +883,7 @@ def cli_preprocess(n_log2):
                             f"BLAKE2b> on a {len(tr)} B transcript file: process start to exit (HIP initialisation, "
                             "transcript digest check, decode + check on the GPU, output file), as the reference's "
                             "binary is run",
-                "wall_s": wall, "points": pts, "points_per_s": pts / wall, "rc": p.returncode,
+                "wall_s": wall, "points": pts, "points_per_s": pts / wall, "rc": p.returncode, "phases": phases,
                 "stdout_tail": p.stdout.strip().splitlines()[-1:] if p.stdout else None,
                 "_out_digest": out_digest}
     finally:

@@ -10,13 +10,15 @@
 //  * no powersoftau_uncompressed intermediate (preprocess-kgz.rs:69-127): the GPU decodes the
 //    compressed transcript straight into the arkworks file.
 // Extra options (for other transcript sizes and synthetic transcripts): --transcript, --out,
-// --n-log2, --gpus, --expect-digest, --no-digest-check, --output-digest. By default the work is the
+// --n-log2, --gpus, --expect-digest, --no-digest-check, --output-digest, --timing. By default the work is the
 // reference's: the transcript's BLAKE2b-512 is checked and the output is not hashed (the reference
 // never hashes it; --output-digest adds that second stream and prints it).
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <sys/stat.h>
+#include <time.h>
+#include <unistd.h>
 
 #include "../../include/kzgpot.h"
 
@@ -33,6 +35,24 @@ const char* kSectionName[] = {"tau_powers_g1", "tau_powers_g2", "alpha_tau_power
                               "beta_g2"};
 constexpr int kPanicExit = 101;  // what a panicking Rust binary exits with
 
+// seconds since this process started (CLOCK_BOOTTIME against /proc/self/stat's start time), for
+// --timing: where a run's wall clock goes before main, in the library call, and after it
+double since_start() {
+  timespec now;
+  clock_gettime(CLOCK_BOOTTIME, &now);
+  double start = 0;
+  if (FILE* f = fopen("/proc/self/stat", "r")) {
+    char buf[1024];
+    const size_t k = fread(buf, 1, sizeof buf - 1, f);
+    fclose(f);
+    buf[k] = 0;
+    const char* q = strrchr(buf, ')');  // field 22 (starttime, clock ticks) counted after the comm field
+    for (int field = 2; q && field < 22; field++) q = strchr(q + 1, ' ');
+    if (q) start = (double)strtoull(q + 1, nullptr, 10) / (double)sysconf(_SC_CLK_TCK);
+  }
+  return (double)now.tv_sec + 1e-9 * (double)now.tv_nsec - start;
+}
+
 [[noreturn]] void panic_exit(const char* msg) {
   fprintf(stderr, "%s\n", msg);
   exit(kPanicExit);
@@ -47,7 +67,8 @@ void usage(const char* prog) {
          "  --gpus N            GPUs to use (default 0 = every visible one)\n"
          "  --expect-digest HEX the transcript's expected BLAKE2b-512 (default: POWERSOFTAU_DIGEST)\n"
          "  --no-digest-check   skip the transcript digest check (transcripts other than the ceremony's)\n"
-         "  --output-digest     also compute and print the output file's BLAKE2b-512\n",
+         "  --output-digest     also compute and print the output file's BLAKE2b-512\n"
+         "  --timing            print seconds since process start at main and around the library call\n",
          prog);
 }
 
@@ -59,7 +80,7 @@ int main(int argc, char** argv) {
   const char* out = "kzg_setup";
   unsigned n_log2 = 21;
   int gpus = 0;
-  bool check_digest = true, output_digest = false;
+  bool check_digest = true, output_digest = false, timing = false;
   const char* expect = kPowersoftauDigest;
   for (int i = 1; i < argc; i++) {
     const bool has_val = i + 1 < argc;
@@ -70,6 +91,7 @@ int main(int argc, char** argv) {
     else if (!strcmp(argv[i], "--expect-digest") && has_val) expect = argv[++i];
     else if (!strcmp(argv[i], "--no-digest-check")) check_digest = false;
     else if (!strcmp(argv[i], "--output-digest")) output_digest = true;
+    else if (!strcmp(argv[i], "--timing")) timing = true;
     else if (!strcmp(argv[i], "-h") || !strcmp(argv[i], "--help")) {
       usage(argv[0]);
       return 0;
@@ -100,6 +122,7 @@ int main(int argc, char** argv) {
              (unsigned long long)want, (unsigned long long)sb.st_size);
     panic_exit(msg);
   }
+  const double t_main = timing ? since_start() : 0;
   if (gpus > 0) printf("Started decompressing + checking Powers of Tau on %d GPU(s)...\n", gpus);
   else printf("Started decompressing + checking Powers of Tau on every visible GPU...\n");
   char tdig[129] = {0}, odig[129] = {0};
@@ -107,6 +130,7 @@ int main(int argc, char** argv) {
   int64_t bad_index = -1;
   const int rc = kzgpot_preprocess_ex(transcript, out, KZGPOT_CLI_MODE, n_log2, gpus, check_digest ? expect : nullptr,
                                       tdig, output_digest ? odig : nullptr, &bad_section, &bad_index);
+  if (timing) printf("timing: main %.3f s after process start, library call done %.3f s after\n", t_main, since_start());
   if (rc == KZGPOT_E_DIGEST) {
     char msg[512];
     snprintf(msg, sizeof msg,
