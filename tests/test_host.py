@@ -181,6 +181,11 @@ def test_cli_reference_failure_paths(mode, tmp_path):
     assert r.returncode == 101
     assert "The size of `powersoftau` should be 296176, but it's 1000, so something isn't right." in r.stderr
     assert not (tmp_path / "kzg_setup").exists()
+    # --expect-digest takes a full BLAKE2b-512 hex digest; anything else is refused up front
+    r = subprocess.run([exe, "--n-log2", "10", "--expect-digest", "abc"], cwd=tmp_path, capture_output=True, text=True)
+    assert r.returncode == 101 and "128 hex characters" in r.stderr
+    r = subprocess.run([exe, "--bogus"], cwd=tmp_path, capture_output=True, text=True)
+    assert r.returncode == 2 and "--output-digest" in r.stdout and "--timing" in r.stdout
 
 
 def test_load_phase1_short_file_is_size_error(kzgpot_mod):
