@@ -156,5 +156,12 @@ int main(int argc, char** argv) {
   printf("transcript BLAKE2b-512: %s\n", tdig);
   if (output_digest) printf("output BLAKE2b-512: %s\n", odig);
   printf("Done serializing. KZG parameters are stored in %s\n", out);
-  return 0;
+  // The output file is complete, closed and renamed into place; what is left is process teardown:
+  // the HIP runtime's exit handlers and the library's pending buffer release. The kernel reclaims
+  // all of it (device queues and memory with the /dev/kfd handle, the mappings with the address
+  // space) whether or not those handlers run, so the binary leaves without them, as a Rust main
+  // that returns leaves without freeing what the OS reclaims.
+  fflush(stdout);
+  fflush(stderr);
+  _exit(0);
 }
