@@ -21,6 +21,7 @@
 #   gather1       bench.py --gather-at-1 (the library's RCCL path at one rank)
 #   port          tests/test_gpu_oracle_port.py alone (every point vs the GPU port of the oracle)
 #   campaign      tools/random_campaign.py for 9 minutes
+#   campaign_g2   the same on the G2 ops only, with fresh seeds
 #   ab_codec      tools/ab_codec.sh (alternating A/B of two library builds)
 #   census        tools/microbench/bin/fpops_peak + tools/fpops/census.py
 set -o pipefail
@@ -58,6 +59,8 @@ for step in "$@"; do
             --timeout-method thread --durations=0 > ${o}_pytest_port.txt 2>&1 ;;
     campaign) timeout -k 10 660 python3 -u tools/random_campaign.py --budget 540 > ${o}_random_campaign.json \
                 2> ${o}_random_campaign.err ;;
+    campaign_g2) timeout -k 10 660 python3 -u tools/random_campaign.py --budget 540 --seed0 200000 \
+                   --ops g2_decompress,g2_transcode > ${o}_random_campaign_g2.json 2> ${o}_random_campaign_g2.err ;;
     ab_codec) timeout -k 10 900 bash tools/ab_codec.sh ;;
     census) timeout -k 10 120 tools/microbench/bin/fpops_peak > ${o}_fpops_peak.txt &&
             timeout -k 10 300 python3 -u tools/fpops/census.py --peaks ${o}_fpops_peak.txt > ${o}_fp_census.json \
