@@ -862,27 +862,36 @@ def cli_preprocess(n_log2):
             if not os.path.exists(exe):
                 rows[f"cli_preprocess_{mode}"] = {"skipped": f"{exe} not built", "_out_digest": None}
                 continue
-            t0 = time.perf_counter()
-            try:
-                p = subprocess.run([exe, "--n-log2", str(n_log2), "--gpus", "1", "--expect-digest", digest,
-                                    "--timing"], cwd=tmpdir, capture_output=True, text=True, timeout=300)
-            except subprocess.TimeoutExpired:
+            runs = []  # two runs: the first also pays the box's cold GPU / driver start, the second is steady
+            for _ in range(2):
+                t0 = time.perf_counter()
+                try:
+                    p = subprocess.run([exe, "--n-log2", str(n_log2), "--gpus", "1", "--expect-digest", digest,
+                                        "--timing"], cwd=tmpdir, capture_output=True, text=True, timeout=300)
+                except subprocess.TimeoutExpired:
+                    p = None
+                    break
+                wall = time.perf_counter() - t0
+                phases = None
+                for ln in (p.stdout or "").splitlines():
+                    if ln.startswith("timing: main "):  # "timing: main A s after process start, library call done B s after"
+                        w = ln.split()
+                        main_s, done_s = float(w[2]), float(w[10])
+                        phases = {"process_start_to_main_s": main_s, "library_call_s": done_s - main_s,
+                                  "after_call_to_exit_s": wall - done_s,
+                                  "note": "start and main from /proc/self/stat (10 ms ticks); exit = wall - call done"}
+                out_digest = None
+                if p.returncode == 0:
+                    with open(dst, "rb") as f:
+                        out_digest = hashlib.blake2b(f.read()).hexdigest()
+                    os.unlink(dst)
+                runs.append((wall, phases, p, out_digest))
+            if p is None or not runs:
                 rows[f"cli_preprocess_{mode}"] = {"skipped": "timed out after 300 s", "_out_digest": None}
                 continue
-            wall = time.perf_counter() - t0
-            phases = None
-            for ln in (p.stdout or "").splitlines():
-                if ln.startswith("timing: main "):  # "timing: main A s after process start, library call done B s after"
-                    w = ln.split()
-                    main_s, done_s = float(w[2]), float(w[10])
-                    phases = {"process_start_to_main_s": main_s, "library_call_s": done_s - main_s,
-                              "after_call_to_exit_s": wall - done_s,
-                              "note": "start and main from /proc/self/stat (10 ms ticks); exit = wall - call done"}
-            out_digest = None
-            if p.returncode == 0:
-                with open(dst, "rb") as f:
-                    out_digest = hashlib.blake2b(f.read()).hexdigest()
-                os.unlink(dst)
+            wall, phases, p, out_digest = runs[-1]
+            if any(r[2].returncode != 0 or r[3] != out_digest for r in runs):
+                out_digest = None  # every run must succeed with the same file
             n = 1 << n_log2
             pts = (2 * n - 1) + 3 * n + 1
             rows[f"cli_preprocess_{mode}"] = {
@@ -890,7 +899,8 @@ def cli_preprocess(n_log2):
                             f"BLAKE2b> on a {len(tr)} B transcript file: process start to exit (HIP initialisation, "
                             "transcript digest check, decode + check on the GPU, output file), as the reference's "
                             "binary is run",
-                "wall_s": wall, "points": pts, "points_per_s": pts / wall, "rc": p.returncode, "phases": phases,
+                "wall_s": wall, "wall_s_each_run": [r[0] for r in runs], "points": pts, "points_per_s": pts / wall,
+                "rc": p.returncode, "phases": phases,
                 "stdout_tail": p.stdout.strip().splitlines()[-1:] if p.stdout else None,
                 "_out_digest": out_digest}
     finally:
