@@ -17,6 +17,7 @@
 #   profile       tools/profile_round.sh TAG (kernel trace --stats + FETCH/WRITE/SQ PMC passes)
 #   asan          tools/asan_gpu_tests.sh (host-ASan library under the C-ABI GPU tests)
 #   loader_stalls tools/pmc_loader_stalls.sh
+#   loader_ceiling tools/microbench/bin/loader_ceiling (the loader's pattern variants, TB/s)
 #   gloo2         bench.py --gpus 2 --dist-backend gloo (the N > 1 launch path on one GPU)
 #   gather1       bench.py --gather-at-1 (the library's RCCL path at one rank)
 #   port          tests/test_gpu_oracle_port.py alone (every point vs the GPU port of the oracle)
@@ -50,6 +51,7 @@ for step in "$@"; do
                   python3 tools/codec_stall_summary.py ${o}_codec_stalls > ${o}_codec_stalls.json ;;
     profile) timeout -k 10 900 bash tools/profile_round.sh $tag ;;
     asan) timeout -k 10 700 bash tools/asan_gpu_tests.sh ;;
+    loader_ceiling) timeout -k 10 400 tools/microbench/bin/loader_ceiling > ${o}_loader_ceiling.txt 2>&1 ;;
     loader_stalls) timeout -k 10 400 bash tools/pmc_loader_stalls.sh ;;
     gloo2) timeout -k 10 400 python bench.py --gpus 2 --dist-backend gloo --g1-log2 24 --steps 2 --warmup 1 \
              --bn254-log2 0 --no-cpu-baseline > ${o}_bench_gloo2.json 2> ${o}_bench_gloo2.err ;;

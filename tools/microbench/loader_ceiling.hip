@@ -23,6 +23,7 @@
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include "../../kzg-setup-powersoftau_amd/csrc/load_kernels.hip"
 
@@ -232,6 +233,32 @@ int main(int argc, char** argv) {
     fflush(stdout);
   };
   const unsigned gs = (unsigned)(n / BLK);
+  {  // the DIN variants must write exactly the product kernel's bytes (G1 over n, G2 over n / 2)
+    const size_t ob = n * 104;
+    uint8_t* want = (uint8_t*)malloc(ob);
+    uint8_t* got = (uint8_t*)malloc(ob);
+    auto cmp = [&](const char* name, auto a, auto b) {
+      CHECK(hipMemset(out, 0xA5, ob));
+      a();
+      CHECK(hipDeviceSynchronize());
+      CHECK(hipMemcpy(want, out, ob, hipMemcpyDeviceToHost));
+      CHECK(hipMemset(out, 0x5A, ob));
+      b();
+      CHECK(hipDeviceSynchronize());
+      CHECK(hipMemcpy(got, out, ob, hipMemcpyDeviceToHost));
+      printf("verify %-14s %s\n", name, memcmp(want, got, ob) == 0 ? "equal" : "DIFFERENT");
+    };
+    cmp("DIN 128 (G1)", [&] { CHECK(kzgpot::launch_load(false, in, out, n, key, nullptr, 0)); }, [&] {
+      hipLaunchKernelGGL((kzgpot::k_load<2, 128, true, 1, true>), dim3((unsigned)(n / 128)), dim3(256), 0, 0, in, out,
+                         n, key, nullptr);
+    });
+    cmp("DIN 32 (G2)", [&] { CHECK(kzgpot::launch_load(true, in, out, n / 2, key, nullptr, 0)); }, [&] {
+      hipLaunchKernelGGL((kzgpot::k_load<4, 32, true, 2, true>), dim3((unsigned)(n / 64)), dim3(64), 0, 0, in, out,
+                         n / 2, key, nullptr);
+    });
+    free(want);
+    free(got);
+  }
   for (int rep = 0; rep < 2; rep++) {
   printf("-- pass %d\n", rep);
   run("copy16", 192.0 * n, [&] { hipLaunchKernelGGL(k_copy16, dim3((unsigned)(n * 6 / 256)), dim3(256), 0, 0, in, out, n * 6); });
@@ -259,6 +286,24 @@ int main(int argc, char** argv) {
   run("k_load 1c/l 64", rw, [&] {
     hipLaunchKernelGGL((kzgpot::k_load<2, 64, true, 1>), dim3((unsigned)(n / 64)), dim3(128), 0, 0, in, out, n, key,
                        nullptr);
+  });
+  // direct input (DIN): lanes read their coordinates straight from global memory, the slab stages
+  // only the output, one block barrier instead of two
+  run("k_load DIN 128", rw, [&] {
+    hipLaunchKernelGGL((kzgpot::k_load<2, 128, true, 1, true>), dim3((unsigned)(n / 128)), dim3(256), 0, 0, in, out, n,
+                       key, nullptr);
+  });
+  run("k_load DIN 64", rw, [&] {
+    hipLaunchKernelGGL((kzgpot::k_load<2, 64, true, 1, true>), dim3((unsigned)(n / 64)), dim3(128), 0, 0, in, out, n,
+                       key, nullptr);
+  });
+  run("k_load DIN 32", rw, [&] {
+    hipLaunchKernelGGL((kzgpot::k_load<2, 32, true, 1, true>), dim3((unsigned)(n / 32)), dim3(64), 0, 0, in, out, n, key,
+                       nullptr);
+  });
+  run("k_load DIN plain 128", rw, [&] {
+    hipLaunchKernelGGL((kzgpot::k_load<2, 128, false, 1, true>), dim3((unsigned)(n / 128)), dim3(256), 0, 0, in, out, n,
+                       key, nullptr);
   });
   run("k_load 2c/l 128", rw, [&] {  // one lane per point, 128 points per block
     hipLaunchKernelGGL((kzgpot::k_load<2, 128, true, 2>), dim3((unsigned)(n / 128)), dim3(128), 0, 0, in, out, n, key,
@@ -297,6 +342,14 @@ int main(int argc, char** argv) {
   run("k_load<G2> 64", (192.0 + 200.0) * n2, [&] {
     hipLaunchKernelGGL((kzgpot::k_load<4, 64, true, 2>), dim3((unsigned)(n2 / 64)), dim3(128), 0, 0, in, out, n2, key,
                        nullptr);
+  });
+  run("k_load<G2> DIN 32", (192.0 + 200.0) * n2, [&] {
+    hipLaunchKernelGGL((kzgpot::k_load<4, 32, true, 2, true>), dim3((unsigned)(n2 / 32)), dim3(64), 0, 0, in, out, n2,
+                       key, nullptr);
+  });
+  run("k_load<G2> DIN 64", (192.0 + 200.0) * n2, [&] {
+    hipLaunchKernelGGL((kzgpot::k_load<4, 64, true, 2, true>), dim3((unsigned)(n2 / 64)), dim3(128), 0, 0, in, out, n2,
+                       key, nullptr);
   });
   run("k_load<G2>plain", (192.0 + 200.0) * n2, [&] {
     hipLaunchKernelGGL((kzgpot::k_load<4, 128, false>), dim3((unsigned)(n2 / 128)), dim3(256), 0, 0, in, out, n2, key,
