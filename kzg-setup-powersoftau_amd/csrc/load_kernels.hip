@@ -83,10 +83,7 @@ KZG_DEV uint4 ld_stream(const uint4* p) {
 }
 KZG_DEV void st_stream(uint4* p, const uint4& v) { __builtin_nontemporal_store((u32x4){v.x, v.y, v.z, v.w}, (u32x4*)p); }
 
-//   DIN = direct input: each lane reads its own coordinates straight from global memory (48-B
-//         pieces at the record stride) instead of from the staged input slab; the slab then only
-//         stages the output, and the block's first barrier goes away.
-template <int NC, int PTS, bool NT = true, int CPL = 2, bool DIN = false>
+template <int NC, int PTS, bool NT = true, int CPL = 2>
 __global__ void __launch_bounds__(PTS * NC / CPL) k_load(const uint4* __restrict__ in, uint4* __restrict__ out,
                                                          uint64_t n, unsigned long long* __restrict__ first_bad,
                                                          uint8_t* __restrict__ status) {
@@ -101,11 +98,9 @@ __global__ void __launch_bounds__(PTS * NC / CPL) k_load(const uint4* __restrict
   const int pt = t / LPP, h = t % LPP;  // this lane: point pt, coordinates CPL h .. CPL h + CPL - 1
 
   const uint4* src = in + base * (RIN / 16);
-  if constexpr (!DIN) {
-    const int nin = cnt * (RIN / 16);
-    for (int k = t; k < nin; k += BLK) slab[k] = NT ? ld_stream(src + k) : src[k];
-    __syncthreads();
-  }
+  const int nin = cnt * (RIN / 16);
+  for (int k = t; k < nin; k += BLK) slab[k] = NT ? ld_stream(src + k) : src[k];
+  __syncthreads();
 
   int st = 0;
   bool finf = false;
@@ -114,19 +109,11 @@ __global__ void __launch_bounds__(PTS * NC / CPL) k_load(const uint4* __restrict
     // ark reads the coordinates in order, and parses the flags before the last one's range
     // check: the lane holding the last coordinate checks its others, the flags, then the last;
     // the first lane of a pair takes precedence (its coordinates come first).
-    const uint4* rec = (DIN ? src : slab) + pt * (RIN / 16) + 3 * CPL * h;
+    const uint4* rec = slab + pt * (RIN / 16) + 3 * CPL * h;
     const bool last = h == LPP - 1;
     words c[CPL];
 #pragma unroll
-    for (int k = 0; k < CPL; k++) {
-      if constexpr (DIN && NT) {
-        const uint4 a = ld_stream(rec + 3 * k), b = ld_stream(rec + 3 * k + 1), d = ld_stream(rec + 3 * k + 2);
-        c[k][0] = a.x, c[k][1] = a.y, c[k][2] = a.z, c[k][3] = a.w, c[k][4] = b.x, c[k][5] = b.y;
-        c[k][6] = b.z, c[k][7] = b.w, c[k][8] = d.x, c[k][9] = d.y, c[k][10] = d.z, c[k][11] = d.w;
-      } else {
-        load_le(c[k], rec + 3 * k);
-      }
-    }
+    for (int k = 0; k < CPL; k++) load_le(c[k], rec + 3 * k);
     const uint32_t yb = c[CPL - 1][11] >> 24;
     const bool fpos = yb & 0x80u;
     finf = last && (yb & 0x40u);
@@ -141,7 +128,7 @@ __global__ void __launch_bounds__(PTS * NC / CPL) k_load(const uint4* __restrict
     const int other = __shfl_xor(st, 1);
     st = h == 0 ? (st ? st : other) : (other ? other : st);
   }
-  if constexpr (!DIN) __syncthreads();  // every lane has read its input record: the slab becomes the output slab
+  __syncthreads();  // every lane has read its input record: the slab becomes the output slab
   if (pt < cnt) {
     uint2* dst = (uint2*)slab + pt * (ROUT / 8) + 6 * CPL * h;
 #pragma unroll

@@ -117,6 +117,65 @@ __global__ void __launch_bounds__(PTS * NC / CPL) k_load_pipe(const uint4* __res
     __syncthreads();  // the slab is read out before the next slab's input overwrites it
   }
 }
+// EXPERIMENT (not in the product; measured slower, profiles/r05i_loader_ceiling.txt): k_load with
+// DIRECT input — each lane reads its own coordinates straight from global memory (48-B pieces at
+// the record stride) instead of from a staged input slab; the slab stages only the output, and
+// the block's first barrier goes away. G1: 5.26 TB/s (5.50 without the nontemporal hint) against
+// 5.61 for the staged product kernel; G2: 3.70 against 5.62.
+template <int NC, int PTS, bool NT, int CPL>
+__global__ void __launch_bounds__(PTS * NC / CPL) k_load_din(const uint4* __restrict__ in, uint4* __restrict__ out,
+                                                             uint64_t n, unsigned long long* __restrict__ first_bad,
+                                                             uint8_t* /* status: not kept */) {
+  constexpr int LPP = NC / CPL, BLK = PTS * LPP;
+  constexpr int RIN = 48 * NC, ROUT = 48 * NC + 8;
+  __shared__ uint4 slab[PTS * ROUT / 16];
+  const uint64_t base = (uint64_t)blockIdx.x * PTS;
+  const int cnt = (int)((n - base) < (uint64_t)PTS ? (n - base) : (uint64_t)PTS);
+  const int t = threadIdx.x, pt = t / LPP, h = t % LPP;
+  int st = 0;
+  bool finf = false;
+  words res[CPL];
+  if (pt < cnt) {
+    const uint4* rec = in + (base + pt) * (RIN / 16) + 3 * CPL * h;
+    const bool last = h == LPP - 1;
+    words c[CPL];
+#pragma unroll
+    for (int k = 0; k < CPL; k++) {
+      uint4 a, b, d;
+      if (NT) a = ld_stream(rec + 3 * k), b = ld_stream(rec + 3 * k + 1), d = ld_stream(rec + 3 * k + 2);
+      else a = rec[3 * k], b = rec[3 * k + 1], d = rec[3 * k + 2];
+      c[k][0] = a.x, c[k][1] = a.y, c[k][2] = a.z, c[k][3] = a.w, c[k][4] = b.x, c[k][5] = b.y;
+      c[k][6] = b.z, c[k][7] = b.w, c[k][8] = d.x, c[k][9] = d.y, c[k][10] = d.z, c[k][11] = d.w;
+    }
+    const uint32_t yb = c[CPL - 1][11] >> 24;
+    const bool fpos = yb & 0x80u;
+    finf = last && (yb & 0x40u);
+    if (last) c[CPL - 1][11] &= 0x3fffffffu;
+    if (CPL == 2 && words_geq_p(c[0])) st = 3;
+    else if (last && fpos && finf) st = 6;
+    else if (words_geq_p(c[CPL - 1])) st = 3;
+#pragma unroll
+    for (int k = 0; k < CPL; k++) words_to_ark_mont(res[k], c[k]);
+  }
+  if (LPP == 2) {
+    const int other = __shfl_xor(st, 1);
+    st = h == 0 ? (st ? st : other) : (other ? other : st);
+  }
+  if (pt < cnt) {
+    uint2* dst = (uint2*)slab + pt * (ROUT / 8) + 6 * CPL * h;
+#pragma unroll
+    for (int k = 0; k < CPL; k++)
+#pragma unroll
+      for (int j = 0; j < 6; j++) dst[6 * k + j] = st ? make_uint2(0, 0) : make_uint2(res[k][2 * j], res[k][2 * j + 1]);
+    if (h == LPP - 1) {
+      dst[6 * CPL] = make_uint2((!st && finf) ? 1u : 0u, 0u);
+      report(base + pt, st, first_bad, nullptr);
+    }
+  }
+  __syncthreads();
+  uint4* dst = (uint4*)((uint8_t*)out + base * ROUT);  // full blocks only (n is a multiple of PTS here)
+  for (int k = t; k < PTS * ROUT / 16; k += BLK) st_stream(dst + k, slab[k]);
+}
 }  // namespace kzgpot
 
 #define CHECK(x)                                                                                 \
@@ -237,7 +296,7 @@ int main(int argc, char** argv) {
     const size_t ob = n * 104;
     uint8_t* want = (uint8_t*)malloc(ob);
     uint8_t* got = (uint8_t*)malloc(ob);
-    auto cmp = [&](const char* name, auto a, auto b) {
+    auto cmp = [&](const char* name, size_t nb, auto a, auto b) {  // the first nb output bytes
       CHECK(hipMemset(out, 0xA5, ob));
       a();
       CHECK(hipDeviceSynchronize());
@@ -246,14 +305,14 @@ int main(int argc, char** argv) {
       b();
       CHECK(hipDeviceSynchronize());
       CHECK(hipMemcpy(got, out, ob, hipMemcpyDeviceToHost));
-      printf("verify %-14s %s\n", name, memcmp(want, got, ob) == 0 ? "equal" : "DIFFERENT");
+      printf("verify %-14s %s\n", name, memcmp(want, got, nb) == 0 ? "equal" : "DIFFERENT");
     };
-    cmp("DIN 128 (G1)", [&] { CHECK(kzgpot::launch_load(false, in, out, n, key, nullptr, 0)); }, [&] {
-      hipLaunchKernelGGL((kzgpot::k_load<2, 128, true, 1, true>), dim3((unsigned)(n / 128)), dim3(256), 0, 0, in, out,
+    cmp("DIN 128 (G1)", n * 104, [&] { CHECK(kzgpot::launch_load(false, in, out, n, key, nullptr, 0)); }, [&] {
+      hipLaunchKernelGGL((kzgpot::k_load_din<2, 128, true, 1>), dim3((unsigned)(n / 128)), dim3(256), 0, 0, in, out,
                          n, key, nullptr);
     });
-    cmp("DIN 32 (G2)", [&] { CHECK(kzgpot::launch_load(true, in, out, n / 2, key, nullptr, 0)); }, [&] {
-      hipLaunchKernelGGL((kzgpot::k_load<4, 32, true, 2, true>), dim3((unsigned)(n / 64)), dim3(64), 0, 0, in, out,
+    cmp("DIN 32 (G2)", n / 2 * 200, [&] { CHECK(kzgpot::launch_load(true, in, out, n / 2, key, nullptr, 0)); }, [&] {
+      hipLaunchKernelGGL((kzgpot::k_load_din<4, 32, true, 2>), dim3((unsigned)(n / 64)), dim3(64), 0, 0, in, out,
                          n / 2, key, nullptr);
     });
     free(want);
@@ -290,19 +349,19 @@ int main(int argc, char** argv) {
   // direct input (DIN): lanes read their coordinates straight from global memory, the slab stages
   // only the output, one block barrier instead of two
   run("k_load DIN 128", rw, [&] {
-    hipLaunchKernelGGL((kzgpot::k_load<2, 128, true, 1, true>), dim3((unsigned)(n / 128)), dim3(256), 0, 0, in, out, n,
+    hipLaunchKernelGGL((kzgpot::k_load_din<2, 128, true, 1>), dim3((unsigned)(n / 128)), dim3(256), 0, 0, in, out, n,
                        key, nullptr);
   });
   run("k_load DIN 64", rw, [&] {
-    hipLaunchKernelGGL((kzgpot::k_load<2, 64, true, 1, true>), dim3((unsigned)(n / 64)), dim3(128), 0, 0, in, out, n,
+    hipLaunchKernelGGL((kzgpot::k_load_din<2, 64, true, 1>), dim3((unsigned)(n / 64)), dim3(128), 0, 0, in, out, n,
                        key, nullptr);
   });
   run("k_load DIN 32", rw, [&] {
-    hipLaunchKernelGGL((kzgpot::k_load<2, 32, true, 1, true>), dim3((unsigned)(n / 32)), dim3(64), 0, 0, in, out, n, key,
+    hipLaunchKernelGGL((kzgpot::k_load_din<2, 32, true, 1>), dim3((unsigned)(n / 32)), dim3(64), 0, 0, in, out, n, key,
                        nullptr);
   });
   run("k_load DIN plain 128", rw, [&] {
-    hipLaunchKernelGGL((kzgpot::k_load<2, 128, false, 1, true>), dim3((unsigned)(n / 128)), dim3(256), 0, 0, in, out, n,
+    hipLaunchKernelGGL((kzgpot::k_load_din<2, 128, false, 1>), dim3((unsigned)(n / 128)), dim3(256), 0, 0, in, out, n,
                        key, nullptr);
   });
   run("k_load 2c/l 128", rw, [&] {  // one lane per point, 128 points per block
@@ -344,11 +403,11 @@ int main(int argc, char** argv) {
                        nullptr);
   });
   run("k_load<G2> DIN 32", (192.0 + 200.0) * n2, [&] {
-    hipLaunchKernelGGL((kzgpot::k_load<4, 32, true, 2, true>), dim3((unsigned)(n2 / 32)), dim3(64), 0, 0, in, out, n2,
+    hipLaunchKernelGGL((kzgpot::k_load_din<4, 32, true, 2>), dim3((unsigned)(n2 / 32)), dim3(64), 0, 0, in, out, n2,
                        key, nullptr);
   });
   run("k_load<G2> DIN 64", (192.0 + 200.0) * n2, [&] {
-    hipLaunchKernelGGL((kzgpot::k_load<4, 64, true, 2, true>), dim3((unsigned)(n2 / 64)), dim3(128), 0, 0, in, out, n2,
+    hipLaunchKernelGGL((kzgpot::k_load_din<4, 64, true, 2>), dim3((unsigned)(n2 / 64)), dim3(128), 0, 0, in, out, n2,
                        key, nullptr);
   });
   run("k_load<G2>plain", (192.0 + 200.0) * n2, [&] {
