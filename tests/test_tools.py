@@ -1,6 +1,7 @@
 """CPU checks of the measurement tools whose output is committed under profiles/: the e2e stage
-summary (tools/stage_summary.py) on a synthetic three-trace run, and the fetch-probe summary's
-request-size arithmetic (tools/fetch_probe_summary.py). No GPU."""
+summary (tools/stage_summary.py) on a synthetic three-trace run, the fetch-probe summary's
+request-size arithmetic (tools/fetch_probe_summary.py) and the codec stall split
+(tools/codec_stall_summary.py). No GPU."""
 import csv
 import json
 import os
@@ -102,3 +103,30 @@ def test_fp_census_matches_the_documented_schedule():
     assert fo["reductions_per_point"] == sum(g1.values())
     assert abs(fo["reductions_per_s"] - sum(g1.values()) * (1 << 27) / 2.12) < 1e3
     assert 0.5 < fo["frac"] < 1.5
+
+
+def test_codec_stall_summary_ratios(tmp_path):
+    """tools/codec_stall_summary.py (profiles/r05a_codec_stalls.json): counters summed per kernel
+    over its dispatches and passes, GRBM_GUI_ACTIVE averaged over the passes that carry it, SQ_WAVES
+    counted once; issue share = 4 x VALU instructions / (GRBM x 128 SIMDs per XCD)."""
+    name = "kzgpot::k_g1_codec(HIP_vector_type<unsigned int, 4u> const*)"
+    passes = {"p1": {"SQ_WAVE_CYCLES": 2000.0, "SQ_WAIT_ANY": 100.0, "SQ_WAIT_INST_ANY": 900.0,
+                     "SQ_ACTIVE_INST_ANY": 1000.0, "SQ_ACTIVE_INST_VALU": 980.0, "GRBM_GUI_ACTIVE": 31.25},
+              "p2": {"SQ_WAVES": 2.0, "SQ_INSTS_VALU": 980.0, "SQ_INSTS_SALU": 10.0, "SQ_INSTS_LDS": 4.0,
+                     "GRBM_GUI_ACTIVE": 31.25},
+              "p3": {"SQ_WAVES": 2.0, "SQ_THREAD_CYCLES_VALU": 980.0 * 64, "SQ_LDS_BANK_CONFLICT": 2.0,
+                     "GRBM_GUI_ACTIVE": 31.25}}
+    for p, counters in passes.items():
+        d = tmp_path / p / "host"
+        d.mkdir(parents=True)
+        # two dispatches per pass, each carrying half of every counter
+        write_csv(d / "run_counter_collection.csv", ["Dispatch_Id", "Kernel_Name", "Counter_Name", "Counter_Value"],
+                  [[k, name, c, v / 2] for k in (1, 2) for c, v in counters.items()])
+    p = subprocess.run([sys.executable, os.path.join(TOOLS, "codec_stall_summary.py"), str(tmp_path)],
+                       capture_output=True, text=True, check=True)
+    k = json.loads(p.stdout)["kernels"]["k_g1_codec"]
+    assert k["waves"] == 2.0 and k["per_wave"]["valu"] == 490.0 and k["per_wave"]["salu"] == 5.0
+    assert k["wait_any_frac"] == 0.05 and k["active_inst_any_frac"] == 0.5
+    assert abs(k["simd_cycles_per_valu"] - 31.25 * 128 / 980) < 1e-12
+    assert abs(k["valu_issue_frac_at_4_cycles"] - 4 * 980 / (31.25 * 128)) < 1e-12
+    assert k["valu_exec_utilisation"] == 1.0 and k["lds_bank_conflict_per_lds_inst"] == 0.5
