@@ -21,7 +21,7 @@
 #   gloo2         bench.py --gpus 2 --dist-backend gloo (the N > 1 launch path on one GPU)
 #   gather1       bench.py --gather-at-1 (the library's RCCL path at one rank)
 #   port          tests/test_gpu_oracle_port.py alone (every point vs the GPU port of the oracle)
-#   campaign      tools/random_campaign.py for 9 minutes
+#   campaign      tools/random_campaign.py for 9 minutes (SEED0=... for fresh seeds)
 #   campaign_g2   the same on the G2 ops only, with fresh seeds
 #   ab_codec      tools/ab_codec.sh (alternating A/B of two library builds)
 #   census        tools/microbench/bin/fpops_peak + tools/fpops/census.py
@@ -59,7 +59,7 @@ for step in "$@"; do
                > ${o}_bench_gather_at_1.json 2> ${o}_bench_gather_at_1.err ;;
     port) timeout -k 10 1000 python -u -m pytest tests/test_gpu_oracle_port.py -x -v --timeout 900 \
             --timeout-method thread --durations=0 > ${o}_pytest_port.txt 2>&1 ;;
-    campaign) timeout -k 10 660 python3 -u tools/random_campaign.py --budget 540 > ${o}_random_campaign.json \
+    campaign) timeout -k 10 660 python3 -u tools/random_campaign.py --budget 540 --seed0 ${SEED0:-1000} > ${o}_random_campaign.json \
                 2> ${o}_random_campaign.err ;;
     campaign_g2) timeout -k 10 660 python3 -u tools/random_campaign.py --budget 540 --seed0 200000 \
                    --ops g2_decompress,g2_transcode > ${o}_random_campaign_g2.json 2> ${o}_random_campaign_g2.err ;;
