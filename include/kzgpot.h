@@ -48,6 +48,11 @@ extern "C" {
 #define KZGPOT_E_NETWORK (-105) /* download requested: this build has no network client */
 #define KZGPOT_E_RANK_FAILED (-106) /* multi-GPU: a rank (maybe this one) could not decode its share */
 #define KZGPOT_E_TIMEOUT (-107)     /* multi-GPU: kzgpot_comm_wait gave up; the communicator is aborted */
+/* Host resources ran out: host memory (std::bad_alloc), the file path's 0.6-1.6 GB buffer mappings,
+ * or a host thread (EAGAIN under a process or thread limit). The call has joined every thread it
+ * started and removed its temporary output file; nothing crossed the C ABI as an exception. The
+ * reference returns a Result here (Accumulator::deserialize, preprocess-kgz.rs:105-110). */
+#define KZGPOT_E_OUT_OF_MEMORY (-108)
 
 /* ---------------------------------------------------------------- flags */
 /* Decompression only (powersoftau CheckForCorrectness::No with no read_g1 afterwards — the βτG1 /
@@ -264,8 +269,8 @@ int kzgpot_comm_wait(void* comm, const uint64_t* d_bad_key, int64_t* first_bad, 
  * KZGPOT_E_DEVICE once the communicator is aborted. bench.py puts these in its line, so an N-GPU
  * number carries RCCL's own proof of N. */
 int kzgpot_comm_size(void* comm, int* nranks, int* rank, int* device);
-/* Failure injection (kzgpot_comm_inject_fault) and the KZGPOT_RCCL_LIB override exist only in the
- * test build libkzgpot_test.so (tests/kzgpot_test_hooks.h); this library binds librccl.so.1. */
+/* Failure injection (kzgpot_comm_inject_fault, kzgpot_test_inject_host_fault) and the
+ * KZGPOT_RCCL_LIB override exist only in the test build libkzgpot_test.so (tests/kzgpot_test_hooks.h); this library binds librccl.so.1. */
 
 /* ---------------------------------------------------------------- misc */
 const char* kzgpot_status_name(int status);  /* name of a KZGPOT_ST_* or KZGPOT_E_* code */

@@ -5,7 +5,9 @@
 #include <stdint.h>
 #include <stdio.h>
 #include <string.h>
+#include <strings.h>
 
+#include <ctype.h>
 #include <errno.h>
 #include <fcntl.h>
 #include <stdlib.h>
@@ -45,6 +47,85 @@ constexpr uint64_t kNoBad = ~0ull;
       return KZGPOT_E_DEVICE;                                                            \
     }                                                                                    \
   } while (0)
+
+// ---------------------------------------------------------------- host resources at the C ABI
+// No exception may cross an extern "C" entry (it would std::terminate the caller's process, where
+// the reference returns a Result, preprocess-kgz.rs:105-110). Host threads are started through
+// start_thread, which reports a failed start (std::system_error EAGAIN under a process or thread
+// limit, std::bad_alloc) as false; every thread body catches its own exceptions; every entry that
+// allocates runs under api_guard; and the threads a call started are joined on every exit path
+// (JoinOnExit, ThreadGroup) before it returns.
+
+#ifdef KZGPOT_TEST_HOOKS
+// Fault injection, test build only (tests/kzgpot_test_hooks.h, kzgpot_test_inject_host_fault):
+// from the (skip + 1)-th event of `site` on, every such event fails until the site is cleared.
+std::atomic<int> g_fault_site{0};
+std::atomic<long> g_fault_skip{0};
+bool injected(int site) {
+  if (g_fault_site.load() != site) return false;
+  return g_fault_skip.fetch_sub(1) <= 0;
+}
+#endif
+enum { kFaultThread = 1, kFaultHostBuf = 2 };
+
+template <class F>
+bool start_thread(std::thread& t, F&& f) noexcept {
+  try {
+#ifdef KZGPOT_TEST_HOOKS
+    if (injected(kFaultThread)) throw std::system_error(EAGAIN, std::generic_category(), "injected thread fault");
+#endif
+    t = std::thread(std::forward<F>(f));
+    return true;
+  } catch (...) {
+    return false;
+  }
+}
+
+template <class F>
+int api_guard(F&& f) noexcept {
+  try {
+    return f();
+  } catch (const std::bad_alloc&) {
+    return KZGPOT_E_OUT_OF_MEMORY;
+  } catch (const std::system_error&) {  // a host thread or lock could not be obtained
+    return KZGPOT_E_OUT_OF_MEMORY;
+  } catch (...) {
+    return KZGPOT_E_DEVICE;
+  }
+}
+
+// Joins a thread on scope exit (after running `before`, e.g. telling it to stop), so that an
+// early return or an exception never destroys a joinable std::thread.
+struct JoinOnExit {
+  std::thread& t;
+  std::function<void()> before;
+  ~JoinOnExit() {
+    if (!t.joinable()) return;
+    if (before) before();
+    t.join();
+  }
+};
+
+// The shard threads of one section: joined on destruction whatever path leaves the scope.
+class ThreadGroup {
+ public:
+  explicit ThreadGroup(size_t n) { th_.reserve(n); }
+  ~ThreadGroup() { join(); }
+  template <class F>
+  bool start(F&& f) noexcept {
+    std::thread t;
+    if (!start_thread(t, std::forward<F>(f))) return false;
+    th_.push_back(std::move(t));  // no reallocation: reserved
+    return true;
+  }
+  void join() {
+    for (auto& t : th_)
+      if (t.joinable()) t.join();
+  }
+
+ private:
+  std::vector<std::thread> th_;
+};
 
 // Per-device staging for the host-buffer API (grown on demand, reused across calls): two slots,
 // each with its own stream, so chunk k's kernel runs while the host thread moves chunk k-1's
@@ -186,6 +267,12 @@ int run_host(int dev, CodecOp op, const uint8_t* in, size_t n, uint8_t* out, uin
     if (!sl.d_key) HIP_TRY(hipMalloc(&sl.d_key, sizeof(unsigned long long)));
   }
   uint64_t best = kNoBad;
+  // an error exit leaves no copy or kernel of this call in flight (the slots are reused)
+  auto quiesce = [&](int code) {
+    for (int k = 0; k < 2; k++)
+      if (c.slot[k].stream) (void)hipStreamSynchronize(c.slot[k].stream);
+    return code;
+  };
   // drain chunk j: its output (and status, key) back to the host
   auto drain = [&](size_t j) -> int {
     TraceRange tr_("kzgpot.d2h");  // waits for chunk j's kernel, then its output copy
@@ -200,7 +287,11 @@ int run_host(int dev, CodecOp op, const uint8_t* in, size_t n, uint8_t* out, uin
     if (key != kNoBad && best == kNoBad) best = ((uint64_t)(key >> 8) + off) << 8 | (key & 0xff);
     if (on_chunk && best == kNoBad) {
       TraceRange tc_("kzgpot.handoff");
-      (*on_chunk)(off, m);
+      try {
+        (*on_chunk)(off, m);
+      } catch (...) {  // the consumer could not queue the range (std::bad_alloc)
+        return quiesce(KZGPOT_E_OUT_OF_MEMORY);
+      }
     }
     return 0;
   };
@@ -210,11 +301,7 @@ int run_host(int dev, CodecOp op, const uint8_t* in, size_t n, uint8_t* out, uin
     span(j, off, m);
     if (in_wait) {
       TraceRange tw_("kzgpot.wait_input");  // the transcript still streaming in from disk
-      if (!(*in_wait)(in + (off + m) * rin)) {  // the transcript read failed
-        for (int k = 0; k < 2; k++)
-          if (c.slot[k].stream) (void)hipStreamSynchronize(c.slot[k].stream);
-        return KZGPOT_E_IO;
-      }
+      if (!(*in_wait)(in + (off + m) * rin)) return quiesce(KZGPOT_E_IO);  // the transcript read failed
     }
     {
       TraceRange th_("kzgpot.h2d");  // a pageable copy: the host thread stages it
@@ -222,9 +309,10 @@ int run_host(int dev, CodecOp op, const uint8_t* in, size_t n, uint8_t* out, uin
     }
     HIP_TRY(hipMemsetAsync(sl.d_key, 0xff, sizeof(unsigned long long), sl.stream));
     HIP_TRY(launch_codec(op, sl.d_in, sl.d_out, m, flags, sl.d_key, status ? sl.d_status : nullptr, sl.stream));
-    if (j > 0 && drain(j - 1)) return KZGPOT_E_DEVICE;  // chunks finish in order: best stays the first
+    if (j > 0)
+      if (const int r = drain(j - 1)) return quiesce(r);  // chunks finish in order: best stays the first
   }
-  if (drain(nchunks - 1)) return KZGPOT_E_DEVICE;
+  if (const int r = drain(nchunks - 1)) return quiesce(r);
   return decode_key(best, first_bad);
 }
 
@@ -250,21 +338,27 @@ extern "C" {
 
 int kzgpot_g1_decompress_ex(const uint8_t* in, size_t n, uint8_t* out, uint32_t flags, int64_t* first_bad,
                             uint8_t* status) {
-  return run_host(current_device(), CodecOp::G1Decompress, in, n, out, flags, first_bad, status);
+  return api_guard(
+      [&] { return run_host(current_device(), CodecOp::G1Decompress, in, n, out, flags, first_bad, status); });
 }
 int kzgpot_g2_decompress_ex(const uint8_t* in, size_t n, uint8_t* out, uint32_t flags, int64_t* first_bad,
                             uint8_t* status) {
-  return run_host(current_device(), CodecOp::G2Decompress, in, n, out, flags, first_bad, status);
+  return api_guard(
+      [&] { return run_host(current_device(), CodecOp::G2Decompress, in, n, out, flags, first_bad, status); });
 }
 int kzgpot_g1_transcode_uncompressed_ex(const uint8_t* in, size_t n, uint8_t* out, uint32_t flags,
                                         int64_t* first_bad, uint8_t* status) {
-  return run_host(current_device(), CodecOp::G1Transcode, in, n, out, flags & KZGPOT_SUBGROUP_REF, first_bad,
-                  status);
+  return api_guard([&] {
+    return run_host(current_device(), CodecOp::G1Transcode, in, n, out, flags & KZGPOT_SUBGROUP_REF, first_bad,
+                    status);
+  });
 }
 int kzgpot_g2_transcode_uncompressed_ex(const uint8_t* in, size_t n, uint8_t* out, uint32_t flags,
                                         int64_t* first_bad, uint8_t* status) {
-  return run_host(current_device(), CodecOp::G2Transcode, in, n, out, flags & KZGPOT_SUBGROUP_REF, first_bad,
-                  status);
+  return api_guard([&] {
+    return run_host(current_device(), CodecOp::G2Transcode, in, n, out, flags & KZGPOT_SUBGROUP_REF, first_bad,
+                    status);
+  });
 }
 int kzgpot_g1_decompress(const uint8_t* in, size_t n, uint8_t* out, uint32_t flags, int64_t* first_bad) {
   return kzgpot_g1_decompress_ex(in, n, out, flags, first_bad, nullptr);
@@ -320,8 +414,11 @@ namespace {
 class OrderedWorker {
  public:
   OrderedWorker(const char* name, std::function<bool(const uint8_t*, size_t)> fn)
-      : name_(name), fn_(std::move(fn)), th_([this] { run(); }) {}
+      : name_(name), fn_(std::move(fn)) {}
   ~OrderedWorker() { finish(); }
+  // false if the thread could not be started (the worker is then unusable)
+  bool start() { return start_thread(th_, [this] { run(); }); }
+  // may throw std::bad_alloc (the queue)
   void push(const uint8_t* p, size_t n) {
     std::lock_guard<std::mutex> l(mu_);
     q_.emplace_back(p, n);
@@ -335,13 +432,17 @@ class OrderedWorker {
       done_ = true;
       cv_.notify_one();
     }
+    if (!th_.joinable()) return ok_ = false;
     th_.join();
     return ok_;
   }
 
  private:
   void run() {
-    trace_thread(name_);
+    try {
+      trace_thread(name_);
+    } catch (...) {
+    }
     for (;;) {
       std::pair<const uint8_t*, size_t> item;
       {
@@ -351,8 +452,12 @@ class OrderedWorker {
         item = q_.front();
         q_.pop_front();
       }
-      TraceRange tr_(name_);
-      if (ok_ && !fn_(item.first, item.second)) ok_ = false;
+      try {
+        TraceRange tr_(name_);
+        if (ok_ && !fn_(item.first, item.second)) ok_ = false;
+      } catch (...) {
+        ok_ = false;
+      }
     }
   }
   const char* name_;
@@ -381,52 +486,49 @@ struct PipelineIo {
   int out_fd = -1;             // >= 0: output ranges are written here (file order offsets) as they land
 };
 
-// The two `main`s (preprocess-kgz.rs:162-199, preprocess-fastkgz.rs:180-213) minus the download.
-// n_shards host threads each decode a contiguous shard of every section; shard g runs on device
-// (current + g) % device_count, so n_shards above the device count oversubscribes (the shards of
-// one device then run one after another) — which is how the multi-shard path is tested on one GPU.
-int preprocess_impl(const uint8_t* tr, size_t len, uint8_t* out, int mode, uint32_t n_log2, int n_shards,
-                    const char* expect_in_hex, char* in_hex, char* out_hex, int* bad_section, int64_t* bad_index,
-                    const PipelineIo& io = PipelineIo()) {
-  if (bad_section) *bad_section = -1;
-  if (bad_index) *bad_index = -1;
-  if (!tr || !out || n_log2 < 1 || n_log2 > 30 || (mode != KZGPOT_MODE_KZG && mode != KZGPOT_MODE_FASTKZG))
-    return KZGPOT_E_INVALID_ARG;
-  if (expect_in_hex && strlen(expect_in_hex) != 128) return KZGPOT_E_INVALID_ARG;
-  if (len != kzgpot_contribution_size(n_log2)) return KZGPOT_E_SIZE;
+// 128 hex digits (either case): the form of expect_transcript_digest
+bool is_hex128(const char* s) {
+  for (int i = 0; i < 128; i++)
+    if (!isxdigit((unsigned char)s[i])) return false;
+  return s[128] == '\0';
+}
 
+int preprocess_run(const uint8_t* tr, size_t len, uint8_t* out, int mode, uint32_t n_log2, int n_shards,
+                   const char* expect_in_hex, char* in_hex, char* out_hex, int* bad_section, int64_t* bad_index,
+                   const PipelineIo& io) {
   // transcript digest (download_parameters' check, preprocess-kgz.rs:51-61) beside the GPU pass;
   // a transcript still streaming from disk is hashed as it arrives. It is the call's critical path
   // (one sequential BLAKE2b stream), so it starts before anything touches HIP: in a fresh process
   // (the CLI drop-ins) the runtime's initialisation then overlaps it instead of preceding it.
   uint8_t in_digest[64];
   bool in_ok = true;
-  std::atomic<bool> abandon{false};  // set when the call fails before the GPU pass starts
+  std::atomic<bool> abandon{false};  // set when the call fails: the hasher stops at its next piece
   std::thread in_hash;
+  JoinOnExit in_hash_join{in_hash, [&abandon] { abandon = true; }};  // any early exit
   const bool want_in = expect_in_hex || in_hex;
   TraceRange call_("kzgpot.preprocess");
-  if (want_in)
-    in_hash = std::thread([&] {
-      trace_thread("kzgpot.blake2b.transcript");
-      TraceRange tr_("kzgpot.blake2b.transcript");
-      Blake2b h;
-      for (size_t off = 0; off < len;) {
-        const size_t m = std::min<size_t>(len - off, (size_t)32 << 20);
-        if (abandon.load(std::memory_order_relaxed) || (io.in_wm && !io.in_wm->wait(off + m))) {
+  if (want_in && !start_thread(in_hash, [&] {
+        try {
+          trace_thread("kzgpot.blake2b.transcript");
+          TraceRange tr_("kzgpot.blake2b.transcript");
+          Blake2b h;
+          for (size_t off = 0; off < len;) {
+            const size_t m = std::min<size_t>(len - off, (size_t)32 << 20);
+            if (abandon.load(std::memory_order_relaxed) || (io.in_wm && !io.in_wm->wait(off + m))) {
+              in_ok = false;
+              return;
+            }
+            h.update(tr + off, m);
+            off += m;
+          }
+          h.finalize(in_digest);
+        } catch (...) {
           in_ok = false;
-          return;
         }
-        h.update(tr + off, m);
-        off += m;
-      }
-      h.finalize(in_digest);
-    });
+      }))
+    return KZGPOT_E_OUT_OF_MEMORY;
   const int ndev = device_count();
-  if (ndev <= 0) {
-    abandon = true;
-    if (in_hash.joinable()) in_hash.join();
-    return KZGPOT_E_DEVICE;
-  }
+  if (ndev <= 0) return KZGPOT_E_DEVICE;
   if (n_shards <= 0) n_shards = ndev;
   n_shards = std::min(n_shards, 64);
   int dev0 = current_device();
@@ -436,14 +538,18 @@ int preprocess_impl(const uint8_t* tr, size_t len, uint8_t* out, int mode, uint3
   // output consumers, fed the file's byte ranges in file order
   Blake2b out_h;
   std::unique_ptr<OrderedWorker> out_hash, out_write;
-  if (out_hex)
+  if (out_hex) {
     out_hash.reset(new OrderedWorker("kzgpot.blake2b.output", [&](const uint8_t* p, size_t m) {
       out_h.update(p, m);
       return true;
     }));
-  if (io.out_fd >= 0)
+    if (!out_hash->start()) return KZGPOT_E_OUT_OF_MEMORY;
+  }
+  if (io.out_fd >= 0) {
     out_write.reset(new OrderedWorker(
         "kzgpot.pwrite", [&](const uint8_t* p, size_t m) { return pwrite_all(io.out_fd, p, m, (uint64_t)(p - out)); }));
+    if (!out_write->start()) return KZGPOT_E_OUT_OF_MEMORY;
+  }
   const bool sink = out_hash || out_write;
   auto push = [&](const uint8_t* p, size_t m) {
     if (out_hash) out_hash->push(p, m);
@@ -473,7 +579,6 @@ int preprocess_impl(const uint8_t* tr, size_t len, uint8_t* out, int mode, uint3
     // contiguous shards, one host thread each
     std::vector<int> rc(n_shards, 0);
     std::vector<int64_t> fb(n_shards, -1);
-    std::vector<std::thread> th;
     const uint64_t per = (cnt[s] + n_shards - 1) / n_shards;
     // The τG1 / ατG1 output (file order) is handed to the digest and writer threads chunk by chunk
     // as it lands, so hashing and writing overlap the GPU pass instead of following it. Each shard
@@ -493,18 +598,29 @@ int preprocess_impl(const uint8_t* tr, size_t len, uint8_t* out, int mode, uint3
         cursor = avail;
       }
     };
-    for (int g = 0; g < n_shards; g++) {
-      const uint64_t lo = std::min(cnt[s], g * per), hi = std::min(cnt[s], lo + per);
-      th.emplace_back([&, g, lo, hi] {
-        trace_thread("kzgpot.shard");
-        TraceRange tr_(kSectionRange[s]);
-        const std::function<void(size_t, size_t)> on_chunk = [&, g](size_t off, size_t m) { land(g, off, m); };
-        rc[g] = run_host((dev0 + g) % ndev, op, p + lo * rin, hi - lo, dst[s] ? dst[s] + lo * rout : nullptr, fl,
-                         &fb[g], nullptr, stream ? &on_chunk : nullptr, dst[s] != nullptr, &in_wait);
-        if (fb[g] >= 0) fb[g] += (int64_t)lo;
-      });
-    }
-    for (auto& t : th) t.join();
+    {
+      // declared after everything the shards use, so it joins them first on any exit
+      ThreadGroup th(n_shards);
+      for (int g = 0; g < n_shards; g++) {
+        const uint64_t lo = std::min(cnt[s], g * per), hi = std::min(cnt[s], lo + per);
+        const bool started = th.start([&, g, lo, hi] {
+          try {
+            trace_thread("kzgpot.shard");
+            TraceRange tr_(kSectionRange[s]);
+            const std::function<void(size_t, size_t)> on_chunk = [&, g](size_t off, size_t m) { land(g, off, m); };
+            rc[g] = run_host((dev0 + g) % ndev, op, p + lo * rin, hi - lo, dst[s] ? dst[s] + lo * rout : nullptr,
+                             fl, &fb[g], nullptr, stream ? &on_chunk : nullptr, dst[s] != nullptr, &in_wait);
+          } catch (...) {
+            rc[g] = KZGPOT_E_OUT_OF_MEMORY;
+          }
+          if (fb[g] >= 0) fb[g] += (int64_t)lo;
+        });
+        if (!started) {  // the shards already running finish their ranges; this one and the rest never run
+          for (int k = g; k < n_shards; k++) rc[k] = KZGPOT_E_OUT_OF_MEMORY;
+          break;
+        }
+      }
+    }  // joined
     // shards are contiguous and in index order: the first failing shard holds the smallest index
     for (int g = 0; g < n_shards && !ret; g++)
       if (rc[g]) {
@@ -553,7 +669,7 @@ int preprocess_impl(const uint8_t* tr, size_t len, uint8_t* out, int mode, uint3
       if (in_hex) memcpy(in_hex, hex, 129);
       // The reference checks the digest before it decodes anything (download_parameters runs
       // first), so a wrong transcript is reported as such even if it also holds a bad point.
-      if (expect_in_hex && strncmp(hex, expect_in_hex, 128) != 0) {
+      if (expect_in_hex && strncasecmp(hex, expect_in_hex, 128) != 0) {
         ret = KZGPOT_E_DIGEST;
         if (bad_section) *bad_section = -1;
         if (bad_index) *bad_index = -1;
@@ -561,6 +677,32 @@ int preprocess_impl(const uint8_t* tr, size_t len, uint8_t* out, int mode, uint3
     }
   }
   return ret;
+}
+
+// The two `main`s (preprocess-kgz.rs:162-199, preprocess-fastkgz.rs:180-213) minus the download.
+// n_shards host threads each decode a contiguous shard of every section; shard g runs on device
+// (current + g) % device_count, so n_shards above the device count oversubscribes (the shards of
+// one device then run one after another) — which is how the multi-shard path is tested on one GPU.
+// Host resources that run out (memory, a thread) end the call with KZGPOT_E_OUT_OF_MEMORY after
+// every thread it started has been joined.
+int preprocess_impl(const uint8_t* tr, size_t len, uint8_t* out, int mode, uint32_t n_log2, int n_shards,
+                    const char* expect_in_hex, char* in_hex, char* out_hex, int* bad_section, int64_t* bad_index,
+                    const PipelineIo& io = PipelineIo()) noexcept {
+  if (bad_section) *bad_section = -1;
+  if (bad_index) *bad_index = -1;
+  if (!tr || !out || n_log2 < 1 || n_log2 > 30 || (mode != KZGPOT_MODE_KZG && mode != KZGPOT_MODE_FASTKZG))
+    return KZGPOT_E_INVALID_ARG;
+  if (expect_in_hex && !is_hex128(expect_in_hex)) return KZGPOT_E_INVALID_ARG;
+  if (len != kzgpot_contribution_size(n_log2)) return KZGPOT_E_SIZE;
+  const int r = api_guard([&] {
+    return preprocess_run(tr, len, out, mode, n_log2, n_shards, expect_in_hex, in_hex, out_hex, bad_section,
+                          bad_index, io);
+  });
+  if (r == KZGPOT_E_OUT_OF_MEMORY) {
+    if (bad_section) *bad_section = -1;
+    if (bad_index) *bad_index = -1;
+  }
+  return r;
 }
 
 }  // namespace
@@ -596,7 +738,12 @@ class HostBuf {
   explicit HostBuf(size_t n) {
     constexpr size_t kHuge = (size_t)2 << 20;
     map_ = n + kHuge;
+#ifdef KZGPOT_TEST_HOOKS
+    void* m = injected(kFaultHostBuf) ? MAP_FAILED
+                                      : mmap(nullptr, map_, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+#else
     void* m = mmap(nullptr, map_, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+#endif
     if (m == MAP_FAILED) {
       map_ = 0;
       return;
@@ -637,14 +784,12 @@ class Releaser {
   void release(std::unique_ptr<HostBuf> a, std::unique_ptr<HostBuf> b) {
     std::lock_guard<std::mutex> l(mu_);
     if (th_.joinable()) th_.join();
-    try {
-      th_ = std::thread([a = std::move(a), b = std::move(b)]() mutable {
-        a.reset();
-        b.reset();
-      });
-    } catch (const std::system_error&) {
-      // the callable (and the buffers it owns) was destroyed with the failed thread: released here
-    }
+    // if no thread starts, the callable (and the buffers it owns) is destroyed with the failed
+    // start: released here, on the calling thread
+    (void)start_thread(th_, [a = std::move(a), b = std::move(b)]() mutable noexcept {
+      a.reset();
+      b.reset();
+    });
   }
 
  private:
@@ -668,59 +813,79 @@ int kzgpot_preprocess_ex(const char* transcript_path, const char* out_path, int 
   if (bad_index) *bad_index = -1;
   if (!transcript_path || !out_path || n_log2 < 1 || n_log2 > 30) return KZGPOT_E_INVALID_ARG;
   TraceRange call_("kzgpot.preprocess_file");
-  const int fd = open(transcript_path, O_RDONLY | O_CLOEXEC);
-  if (fd < 0) return KZGPOT_E_IO;
-  const off_t flen = lseek(fd, 0, SEEK_END);
-  if (flen < 0 || (uint64_t)flen != kzgpot_contribution_size(n_log2)) {
-    close(fd);
-    return flen < 0 ? KZGPOT_E_IO : KZGPOT_E_SIZE;
-  }
-  const size_t len = (size_t)flen;
-  (void)posix_fadvise(fd, 0, flen, POSIX_FADV_SEQUENTIAL);
-  int r = 0;
-  std::string tmp = std::string(out_path) + ".kzgpot-tmp-XXXXXX";
-  {
-    std::unique_ptr<HostBuf> tr(new HostBuf(len)), out(new HostBuf(kzgpot_output_size(n_log2, mode)));
-    if (!tr->get() || !out->get()) {
-      close(fd);
-      return KZGPOT_E_INVALID_ARG;
+  // Everything the call opens, creates or starts is undone on every exit path, including an
+  // exception (std::bad_alloc) caught by api_guard below: the reader is joined, both descriptors
+  // closed, and the temporary output removed unless it was renamed over out_path.
+  struct Files {
+    int fd = -1, ofd = -1;
+    std::string tmp;
+    bool committed = false;
+    ~Files() {
+      if (fd >= 0) close(fd);
+      if (ofd >= 0) close(ofd);
+      if (!tmp.empty() && !committed) unlink(tmp.c_str());
     }
+  };
+  std::unique_ptr<HostBuf> tr, out;
+  const int ret = api_guard([&]() -> int {
+    Files f;
+    f.fd = open(transcript_path, O_RDONLY | O_CLOEXEC);
+    if (f.fd < 0) return KZGPOT_E_IO;
+    const off_t flen = lseek(f.fd, 0, SEEK_END);
+    if (flen < 0) return KZGPOT_E_IO;
+    if ((uint64_t)flen != kzgpot_contribution_size(n_log2)) return KZGPOT_E_SIZE;
+    const size_t len = (size_t)flen;
+    (void)posix_fadvise(f.fd, 0, flen, POSIX_FADV_SEQUENTIAL);
+    tr.reset(new HostBuf(len));
+    out.reset(new HostBuf(kzgpot_output_size(n_log2, mode)));
+    if (!tr->get() || !out->get()) return KZGPOT_E_OUT_OF_MEMORY;  // the 0.6-1.6 GB mappings
     // unique per call (mkstemp), so concurrent calls for one out_path never share a temporary
-    const int ofd = mkostemp(&tmp[0], O_CLOEXEC);
-    if (ofd < 0) {
-      close(fd);
-      return KZGPOT_E_IO;
-    }
-    (void)fchmod(ofd, 0644);  // mkstemp creates 0600: a setup file is meant to be read by others
+    std::string tmp = std::string(out_path) + ".kzgpot-tmp-XXXXXX";
+    f.ofd = mkostemp(&tmp[0], O_CLOEXEC);
+    if (f.ofd < 0) return KZGPOT_E_IO;
+    f.tmp.swap(tmp);
+    (void)fchmod(f.ofd, 0644);  // mkstemp creates 0600: a setup file is meant to be read by others
     Watermark wm;
-    std::thread reader([&] {
-      trace_thread("kzgpot.pread");
-      TraceRange tr_("kzgpot.pread");
-      for (size_t off = 0; off < len && !wm.failed();) {  // stops at the next piece once the pipeline failed
-        const ssize_t k = pread(fd, tr->get() + off, std::min<size_t>(len - off, (size_t)32 << 20), (off_t)off);
-        if (k < 0 && errno == EINTR) continue;
-        if (k <= 0) return wm.fail();
-        off += (size_t)k;
-        wm.advance(off);
-      }
-    });
+    std::thread reader;
+    JoinOnExit reader_join{reader, [&wm] { wm.fail(); }};  // stops at its next piece, then joined
+    uint8_t* const trp = tr->get();
+    const int fd = f.fd;
+    if (!start_thread(reader, [&wm, trp, fd, len]() noexcept {
+          try {
+            trace_thread("kzgpot.pread");
+          } catch (...) {
+          }
+          // stops at the next piece once the pipeline failed
+          for (size_t off = 0; off < len && !wm.failed();) {
+            const ssize_t k = pread(fd, trp + off, std::min<size_t>(len - off, (size_t)32 << 20), (off_t)off);
+            if (k < 0 && errno == EINTR) continue;
+            if (k <= 0) return wm.fail();
+            off += (size_t)k;
+            wm.advance(off);
+          }
+        }))
+      return KZGPOT_E_OUT_OF_MEMORY;
     PipelineIo io;
     io.in_wm = &wm;
-    io.out_fd = ofd;
-    r = preprocess_impl(tr->get(), len, out->get(), mode, n_log2, n_gpus, expect_transcript_digest,
-                        transcript_digest, output_digest, bad_section, bad_index, io);
+    io.out_fd = f.ofd;
+    int r = preprocess_impl(trp, len, out->get(), mode, n_log2, n_gpus, expect_transcript_digest, transcript_digest,
+                            output_digest, bad_section, bad_index, io);
     if (r) wm.fail();  // the reader finishes its current pread and stops; nothing waits on it
     reader.join();
-    {
-      TraceRange fin_("kzgpot.file_finish");  // closes and rename
-      close(fd);
-      if (close(ofd) != 0 && !r) r = KZGPOT_E_IO;
-      if (!r && rename(tmp.c_str(), out_path) != 0) r = KZGPOT_E_IO;
-      if (r) unlink(tmp.c_str());
-    }
-    g_release.release(std::move(tr), std::move(out));  // unmapped behind the return (Releaser)
+    TraceRange fin_("kzgpot.file_finish");  // closes and rename
+    const int ofd = f.ofd;
+    f.ofd = -1;
+    if (close(ofd) != 0 && !r) r = KZGPOT_E_IO;
+    if (!r && rename(f.tmp.c_str(), out_path) != 0) r = KZGPOT_E_IO;
+    f.committed = r == 0;
+    return r;
+  });
+  if (tr || out) g_release.release(std::move(tr), std::move(out));  // unmapped behind the return (Releaser)
+  if (ret == KZGPOT_E_OUT_OF_MEMORY) {
+    if (bad_section) *bad_section = -1;
+    if (bad_index) *bad_index = -1;
   }
-  return r;
+  return ret;
 }
 int kzgpot_preprocess(const char* transcript_path, const char* out_path, int mode, uint32_t n_log2, int n_gpus,
                       int* bad_section, int64_t* bad_index) {
@@ -730,11 +895,11 @@ int kzgpot_preprocess(const char* transcript_path, const char* out_path, int mod
 // ------------------------------------------------------------------------------- loader mirror
 int kzgpot_g1_deserialize_unchecked_ex(const uint8_t* in, size_t n, uint8_t* out, int64_t* first_bad,
                                        uint8_t* status) {
-  return run_host(current_device(), CodecOp::G1Load, in, n, out, 0, first_bad, status);
+  return api_guard([&] { return run_host(current_device(), CodecOp::G1Load, in, n, out, 0, first_bad, status); });
 }
 int kzgpot_g2_deserialize_unchecked_ex(const uint8_t* in, size_t n, uint8_t* out, int64_t* first_bad,
                                        uint8_t* status) {
-  return run_host(current_device(), CodecOp::G2Load, in, n, out, 0, first_bad, status);
+  return api_guard([&] { return run_host(current_device(), CodecOp::G2Load, in, n, out, 0, first_bad, status); });
 }
 int kzgpot_g1_deserialize_unchecked(const uint8_t* in, size_t n, uint8_t* out, int64_t* first_bad) {
   return kzgpot_g1_deserialize_unchecked_ex(in, n, out, first_bad, nullptr);
@@ -747,7 +912,7 @@ int kzgpot_g1_deserialize_unchecked_dev(const void* d_in, size_t n, void* d_out,
   return run_dev(CodecOp::G1Load, d_in, n, d_out, 0, d_bad_key, d_status, stream);
 }
 int kzgpot_bn254_g1_decompress_ex(const uint8_t* in, size_t n, uint8_t* out, int64_t* first_bad, uint8_t* status) {
-  return run_host(current_device(), CodecOp::Bn254G1Decompress, in, n, out, 0, first_bad, status);
+  return api_guard([&] { return run_host(current_device(), CodecOp::Bn254G1Decompress, in, n, out, 0, first_bad, status); });
 }
 int kzgpot_bn254_g1_decompress(const uint8_t* in, size_t n, uint8_t* out, int64_t* first_bad) {
   return kzgpot_bn254_g1_decompress_ex(in, n, out, first_bad, nullptr);
@@ -809,7 +974,12 @@ int read_file(const char* path, std::vector<uint8_t>& buf) {
     fclose(f);
     return KZGPOT_E_IO;
   }
-  buf.resize((size_t)len);
+  try {
+    buf.resize((size_t)len);
+  } catch (const std::bad_alloc&) {
+    fclose(f);
+    return KZGPOT_E_OUT_OF_MEMORY;
+  }
   const size_t got = fread(buf.data(), 1, buf.size(), f);
   fclose(f);
   return got == buf.size() ? 0 : KZGPOT_E_IO;
@@ -829,15 +999,17 @@ int kzgpot_load_kzg_setup_buffer(const uint8_t* file, size_t len, uint32_t n_log
       {CodecOp::G1Load, 2, vk, 2},                       // VerifierKey g, gamma_g
       {CodecOp::G2Load, 2, vk + 2 * g1, 2},              // VerifierKey h, beta_h
   };
-  return load_sections(file, len, secs, 4, bad_section, bad_index);
+  return api_guard([&] { return load_sections(file, len, secs, 4, bad_section, bad_index); });
 }
 int kzgpot_load_kzg_setup(const char* path, uint32_t n_log2, uint8_t* powers_of_g, uint8_t* powers_of_gamma_g,
                           uint8_t* vk, int* bad_section, int64_t* bad_index) {
-  std::vector<uint8_t> buf;
-  const int r = read_file(path, buf);
-  if (r) return r;
-  return kzgpot_load_kzg_setup_buffer(buf.data(), buf.size(), n_log2, powers_of_g, powers_of_gamma_g, vk,
-                                      bad_section, bad_index);
+  return api_guard([&] {
+    std::vector<uint8_t> buf;
+    const int r = read_file(path, buf);
+    if (r) return r;
+    return kzgpot_load_kzg_setup_buffer(buf.data(), buf.size(), n_log2, powers_of_g, powers_of_gamma_g, vk,
+                                        bad_section, bad_index);
+  });
 }
 uint64_t kzgpot_phase1_size(uint32_t exp) {
   if (exp > 30) return 0;
@@ -858,16 +1030,18 @@ int kzgpot_load_phase1_buffer(const uint8_t* file, size_t len, uint32_t exp, uin
       {CodecOp::G1Phase1, m, alpha_coeffs_g1, 5},  // src/lib.rs:103-106
       {CodecOp::G1Phase1, m, beta_coeffs_g1, 6},   // src/lib.rs:107-110
   };
-  return load_sections(file, len, secs, 7, bad_section, bad_index);
+  return api_guard([&] { return load_sections(file, len, secs, 7, bad_section, bad_index); });
 }
 int kzgpot_load_phase1(const char* path, uint32_t exp, uint8_t* alpha, uint8_t* beta_g1, uint8_t* beta_g2,
                        uint8_t* coeffs_g1, uint8_t* coeffs_g2, uint8_t* alpha_coeffs_g1, uint8_t* beta_coeffs_g1,
                        int* bad_section, int64_t* bad_index) {
-  std::vector<uint8_t> buf;
-  const int r = read_file(path, buf);
-  if (r) return r;
-  return kzgpot_load_phase1_buffer(buf.data(), buf.size(), exp, alpha, beta_g1, beta_g2, coeffs_g1, coeffs_g2,
-                                   alpha_coeffs_g1, beta_coeffs_g1, bad_section, bad_index);
+  return api_guard([&] {
+    std::vector<uint8_t> buf;
+    const int r = read_file(path, buf);
+    if (r) return r;
+    return kzgpot_load_phase1_buffer(buf.data(), buf.size(), exp, alpha, beta_g1, beta_g2, coeffs_g1, coeffs_g2,
+                                     alpha_coeffs_g1, beta_coeffs_g1, bad_section, bad_index);
+  });
 }
 int kzgpot_load_fastkzg_setup_buffer(const uint8_t* file, size_t len, uint32_t n_log2, uint8_t* powers_of_g,
                                      uint8_t* powers_of_gamma_g, uint8_t* h_beta_h, uint8_t* powers_of_h,
@@ -880,15 +1054,17 @@ int kzgpot_load_fastkzg_setup_buffer(const uint8_t* file, size_t len, uint32_t n
       {CodecOp::G2Load, 2, h_beta_h, 2},             // h, beta_h (src/lib.rs:211-212)
       {CodecOp::G2Load, n, powers_of_h, 3},          // src/lib.rs:214-217
   };
-  return load_sections(file, len, secs, 4, bad_section, bad_index);
+  return api_guard([&] { return load_sections(file, len, secs, 4, bad_section, bad_index); });
 }
 int kzgpot_load_fastkzg_setup(const char* path, uint32_t n_log2, uint8_t* powers_of_g, uint8_t* powers_of_gamma_g,
                               uint8_t* h_beta_h, uint8_t* powers_of_h, int* bad_section, int64_t* bad_index) {
-  std::vector<uint8_t> buf;
-  const int r = read_file(path, buf);
-  if (r) return r;
-  return kzgpot_load_fastkzg_setup_buffer(buf.data(), buf.size(), n_log2, powers_of_g, powers_of_gamma_g,
-                                          h_beta_h, powers_of_h, bad_section, bad_index);
+  return api_guard([&] {
+    std::vector<uint8_t> buf;
+    const int r = read_file(path, buf);
+    if (r) return r;
+    return kzgpot_load_fastkzg_setup_buffer(buf.data(), buf.size(), n_log2, powers_of_g, powers_of_gamma_g,
+                                            h_beta_h, powers_of_h, bad_section, bad_index);
+  });
 }
 
 const char* kzgpot_status_name(int s) {
@@ -909,10 +1085,22 @@ const char* kzgpot_status_name(int s) {
     case KZGPOT_E_NETWORK: return "NetworkUnavailable";
     case KZGPOT_E_RANK_FAILED: return "RankFailed";
     case KZGPOT_E_TIMEOUT: return "Timeout";
+    case KZGPOT_E_OUT_OF_MEMORY: return "OutOfMemory";
     default: return "unknown";
   }
 }
 int kzgpot_device_count(void) { return device_count(); }
 const char* kzgpot_version(void) { return "kzgpot 0.1.0 (gfx950)"; }
+
+#ifdef KZGPOT_TEST_HOOKS
+// test build only (tests/kzgpot_test_hooks.h)
+int kzgpot_test_inject_host_fault(int site, long skip) {
+  if (site < 0 || site > kFaultHostBuf || skip < 0) return KZGPOT_E_INVALID_ARG;
+  g_fault_site = 0;
+  g_fault_skip = skip;
+  g_fault_site = site;
+  return 0;
+}
+#endif
 
 }  // extern "C"

@@ -36,6 +36,7 @@
 
 #include <chrono>
 #include <mutex>
+#include <new>
 #include <thread>
 #include <vector>
 
@@ -170,6 +171,11 @@ __global__ void k_merge_keys(const unsigned long long* __restrict__ keys, uint32
 }
 
 int ensure_events(Comm& c, size_t need) {
+  try {
+    c.ev.reserve(need);  // push_back below cannot throw then
+  } catch (const std::bad_alloc&) {  // never across the C ABI: the caller still issues its collectives
+    return KZGPOT_E_OUT_OF_MEMORY;
+  }
   while (c.ev.size() < need) {
     hipEvent_t e;
     HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -208,7 +214,8 @@ int kzgpot_comm_init(void** comm, const uint8_t* id, int nranks, int rank) {
   if (!rccl().ok) return KZGPOT_E_DEVICE;
   int dev = -1;
   HIP_OK(hipGetDevice(&dev));
-  Comm* c = new Comm;
+  Comm* c = new (std::nothrow) Comm;
+  if (!c) return KZGPOT_E_OUT_OF_MEMORY;
   c->rank = rank;
   c->nranks = nranks;
   c->device = dev;

@@ -13,6 +13,7 @@
 // --n-log2, --gpus, --expect-digest, --no-digest-check, --output-digest, --timing. By default the work is the
 // reference's: the transcript's BLAKE2b-512 is checked and the output is not hashed (the reference
 // never hashes it; --output-digest adds that second stream and prints it).
+#include <ctype.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -101,7 +102,16 @@ int main(int argc, char** argv) {
     }
   }
   if (n_log2 < 1 || n_log2 > 28) panic_exit("--n-log2 must be in 1..28");
+  // checked up front (and normalised to the library's lowercase hex), so that a mistyped digest is
+  // reported as such instead of as a failed validation after the whole transcript is hashed
+  char expect_lc[129];
   if (strlen(expect) != 128) panic_exit("--expect-digest must be 128 hex characters");
+  for (int i = 0; i < 128; i++) {
+    if (!isxdigit((unsigned char)expect[i])) panic_exit("--expect-digest must be 128 hex characters");
+    expect_lc[i] = (char)tolower((unsigned char)expect[i]);
+  }
+  expect_lc[128] = '\0';
+  expect = expect_lc;
 
   // download_parameters (preprocess-kgz.rs:32-67): only the "existing file" branch exists here
   struct stat sb;

@@ -21,6 +21,15 @@ extern "C" {
 #define KZGPOT_FAULT_LAUNCH 1
 #define KZGPOT_FAULT_COLLECTIVE 2
 int kzgpot_comm_inject_fault(void* comm, int site, uint32_t at);
+/* Host-resource failure injection (csrc/capi.hip): from the (skip + 1)-th event of `site` on, every
+ * such event in the process fails, until site 0 clears it:
+ *   KZGPOT_HOST_FAULT_THREAD: a library host thread fails to start, as std::thread does with
+ *   std::system_error(EAGAIN) under RLIMIT_NPROC; KZGPOT_HOST_FAULT_HOSTBUF: the file path's
+ *   large anonymous mapping fails (mmap MAP_FAILED). The entry points must return
+ *   KZGPOT_E_OUT_OF_MEMORY with every started thread joined and no temporary file left. */
+#define KZGPOT_HOST_FAULT_THREAD 1
+#define KZGPOT_HOST_FAULT_HOSTBUF 2
+int kzgpot_test_inject_host_fault(int site, long skip);
 #ifdef __cplusplus
 }
 #endif
