@@ -33,6 +33,7 @@ import argparse
 import ctypes
 import json
 import os
+import shutil
 import sys
 import tempfile
 import time
@@ -259,43 +260,44 @@ def cpu_e2e(n_log2, seed, dev, D, kzgpot, gpu_rows):
     pts = (2 * n - 1) + 3 * n + 1
     tr, _ = e2e_transcript(n_log2, seed, dev, D)
     tmpdir = tempfile.mkdtemp(prefix="kzgpot_cpu_e2e_")
-    src = os.path.join(tmpdir, "powersoftau")
-    tr.tofile(src)
-    digest = hashlib.blake2b(tr.tobytes()).hexdigest()
-    cores = num_cpus()
-    glib = _lib.load()
-    rows = {}
-    for mode, name in ((kzgpot.MODE_KZG, "kgz"), (kzgpot.MODE_FASTKZG, "fastkgz")):
-        unc, dst, gdst = (os.path.join(tmpdir, x) for x in ("powersoftau_uncompressed", "out", "gpu_out"))
-        stages = (ctypes.c_double * 5)()
-        t = time.perf_counter()
-        r = lib.oracle_preprocess_pipeline(src.encode(), unc.encode(), dst.encode(), ctypes.c_uint64(n), mode, cores,
-                                           digest.encode(), None, stages)
-        dt = time.perf_counter() - t
-        sec, idx = ctypes.c_int(-1), ctypes.c_int64(-1)
-        rg = glib.kzgpot_preprocess_ex(src.encode(), gdst.encode(), mode, n_log2, 1, digest.encode(), None, None,
-                                       ctypes.byref(sec), ctypes.byref(idx))
-        same = r == 0 and rg == 0 and np.array_equal(np.fromfile(dst, np.uint8), np.fromfile(gdst, np.uint8))
-        for f in (unc, dst, gdst):
-            if os.path.exists(f):
-                os.unlink(f)
-        st = list(stages)
-        # per-point cost of each stage, scaled to the reference's N = 2^21 (every stage is linear in N)
-        scale = ((2 << 21) - 1 + 3 * (1 << 21) + 1) / pts
-        gpu = gpu_rows.get(f"preprocess_{name}_e2e_file_transcript_digest") if gpu_rows else None
-        rows[name] = {
-            "n_log2": n_log2, "points": pts, "seconds": dt, "points_per_s": pts / dt, "rc": r,
-            "threads_decompress": cores, "threads_check": 1,
-            "stages_s": {"transcript_blake2b_check": st[0], "read_hash_decompress": st[1],
-                         "write_uncompressed_intermediate": st[2], "read_g1_g2_subgroup_check": st[3],
-                         "write_output_unbuffered": st[4]},
-            "extrapolated_s_at_2e21": dt * scale,
-            "output_equal_to_gpu_kzgpot_preprocess_ex": bool(same),
-            "gpu_row": None if gpu is None else {"row": f"next_rows.preprocess_{name}_e2e_file_transcript_digest",
-                                                 "points_per_s": gpu["points_per_s"],
-                                                 "speedup_per_point": gpu["points_per_s"] / (pts / dt)}}
-    os.unlink(src)
-    os.rmdir(tmpdir)
+    try:  # the temporary directory goes whatever happens in between
+        src = os.path.join(tmpdir, "powersoftau")
+        tr.tofile(src)
+        digest = hashlib.blake2b(tr.tobytes()).hexdigest()
+        cores = num_cpus()
+        glib = _lib.load()
+        rows = {}
+        for mode, name in ((kzgpot.MODE_KZG, "kgz"), (kzgpot.MODE_FASTKZG, "fastkgz")):
+            unc, dst, gdst = (os.path.join(tmpdir, x) for x in ("powersoftau_uncompressed", "out", "gpu_out"))
+            stages = (ctypes.c_double * 5)()
+            t = time.perf_counter()
+            r = lib.oracle_preprocess_pipeline(src.encode(), unc.encode(), dst.encode(), ctypes.c_uint64(n), mode, cores,
+                                               digest.encode(), None, stages)
+            dt = time.perf_counter() - t
+            sec, idx = ctypes.c_int(-1), ctypes.c_int64(-1)
+            rg = glib.kzgpot_preprocess_ex(src.encode(), gdst.encode(), mode, n_log2, 1, digest.encode(), None, None,
+                                           ctypes.byref(sec), ctypes.byref(idx))
+            same = r == 0 and rg == 0 and np.array_equal(np.fromfile(dst, np.uint8), np.fromfile(gdst, np.uint8))
+            for f in (unc, dst, gdst):
+                if os.path.exists(f):
+                    os.unlink(f)
+            st = list(stages)
+            # per-point cost of each stage, scaled to the reference's N = 2^21 (every stage is linear in N)
+            scale = ((2 << 21) - 1 + 3 * (1 << 21) + 1) / pts
+            gpu = gpu_rows.get(f"preprocess_{name}_e2e_file_transcript_digest") if gpu_rows else None
+            rows[name] = {
+                "n_log2": n_log2, "points": pts, "seconds": dt, "points_per_s": pts / dt, "rc": r,
+                "threads_decompress": cores, "threads_check": 1,
+                "stages_s": {"transcript_blake2b_check": st[0], "read_hash_decompress": st[1],
+                             "write_uncompressed_intermediate": st[2], "read_g1_g2_subgroup_check": st[3],
+                             "write_output_unbuffered": st[4]},
+                "extrapolated_s_at_2e21": dt * scale,
+                "output_equal_to_gpu_kzgpot_preprocess_ex": bool(same),
+                "gpu_row": None if gpu is None else {"row": f"next_rows.preprocess_{name}_e2e_file_transcript_digest",
+                                                     "points_per_s": gpu["points_per_s"],
+                                                     "speedup_per_point": gpu["points_per_s"] / (pts / dt)}}
+    finally:
+        shutil.rmtree(tmpdir, ignore_errors=True)
     return {"unit": "points/s", "kind": "port", "cores": cores,
             "sample": f"N = 2^{n_log2} synthetic response transcript ({tr.size} B) file to file per mode, the "
                       "reference's pipeline shape (oracle_preprocess_pipeline); stage times linear in N",

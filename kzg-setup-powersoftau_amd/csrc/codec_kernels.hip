@@ -43,26 +43,33 @@ namespace kzgpot {
 // ================================================================================ phase 1: G2
 // Fp2 square root without Algorithm 9's data-dependent branches (any root works: the sign
 // rule normalises it). With N = a0^2 + a1^2 (a is a square in Fp2 iff N is one in Fp):
-//   gam = sqrt(N); d = (a0 + gam)/2 (d = a0 if that is 0); t = d^((p-3)/4); s = t d
+//   gam = N^((p+1)/4); d = (a0 + gam)/2 (d = a0 if that is 0); t = d^((p-3)/4); s = t d
 //   s^2 == d  ->  y = (s, a1 t / 2)      else (s^2 = -d, t s = -1)  ->  y = (-a1 t / 2, s)
-// and y is accepted iff y^2 == a (no separate gam^2 == N test: a non-square a has no y with
-// y^2 = a, and a square a has a square norm). Two Fp exponentiations (~920 Fp multiplies) where
-// Algorithm 9 needs two Fp2 ones (~2,700). In: a reduced; out: y reduced.
+// and a is accepted iff gam^2 == N. That one Fp squaring decides exactly what y^2 == a would
+// (an Fp2 squaring, two subtractions and two zero tests, ~1.6 K VALU instructions more): for
+// d != 0 both cases give y^2 = d - a1^2 / (4d) + a1 u, whose real part is a0 iff
+// (a0 + gam)^2 - 2 a0 (a0 + gam) - a1^2 = gam^2 - N = 0; for d = a0 + gam = 0 (so gam = -a0) the
+// fallback d = a0 gives y^2 = a iff a1 = 0 iff gam^2 = a0^2 = N (and a0 = 0 forces a = 0, y = 0).
+// tests/test_fast_paths_math.py checks the equivalence against Algorithm 9. The halvings are
+// fp_half (a shift) instead of multiplies by 1/2. Two Fp exponentiations (~920 Fp multiplies)
+// where Algorithm 9 needs two Fp2 ones (~2,700). In: a reduced; out: y reduced.
 KZG_DEV bool fp2_sqrt(fp2& y, const fp2& a) {
-  fp nrm, t0, gam, d, s, h, inv2;
+  fp nrm, t0, gam, d, s, h;
   fp_sqr(nrm, a.c0);
   fp_sqr(t0, a.c1);
   fp_add_nr(nrm, nrm, t0);
   fp_pow_pm3d4(t0, nrm);
   fp_mul(gam, t0, nrm);
-  fp_set(inv2, FP_INV2);
+  fp_sqr(t0, gam);
+  const bool square = fp_eq(t0, nrm);  // gam^2 == N
   fp_add_nr(d, a.c0, gam);
-  fp_mul(d, d, inv2);
+  fp_norm(d, d);
+  fp_half(d, d);  // (a0 + gam) / 2
   fp_select(d, fp_is_zero(d), a.c0, d);
   fp_pow_pm3d4(t0, d);  // t
   fp_mul(s, t0, d);
-  fp_mul(h, a.c1, t0);
-  fp_mul(h, h, inv2);
+  fp_half(h, a.c1);
+  fp_mul(h, h, t0);  // a1 t / 2
   fp_sqr(t0, s);
   const bool case1 = fp_eq(t0, d);
   fp nh;
@@ -70,11 +77,7 @@ KZG_DEV bool fp2_sqrt(fp2& y, const fp2& a) {
   fp_sub_red(nh, nh, h);
   fp_select(y.c0, case1, s, nh);
   fp_select(y.c1, case1, h, s);
-  fp2 y2;
-  f_sqr(y2, y);
-  fp_sub_red(y2.c0, y2.c0, a.c0);
-  fp_sub_red(y2.c1, y2.c1, a.c1);
-  return f_is_zero(y2);
+  return square;
 }
 
 // x^3 + 4 (1 + u), reduced
@@ -172,7 +175,7 @@ __global__ void __launch_bounds__(kBlock) k_g2_decompress(const uint4* __restric
 // free until the emit), the ark record goes out in one go after the sign rule, and y's Montgomery
 // form replaces the words. The ladder reads the base point from LDS. The split path's check
 // re-reads the 192-B record, converts four coordinates and tests the curve equation; here the
-// point is on the curve by construction (fp2_sqrt verified y^2 = x^3 + 4 (1 + u)) and only y is
+// point is on the curve by construction (fp2_sqrt accepts only when y^2 = x^3 + 4 (1 + u)) and only y is
 // converted. 56 KB of LDS per block.
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 2)))
 k_g2_codec(const uint4* __restrict__ in, uint4* __restrict__ out, uint64_t n, uint32_t flags,
@@ -232,8 +235,15 @@ k_g2_codec(const uint4* __restrict__ in, uint4* __restrict__ out, uint64_t n, ui
       store_words(dst + 3, w1);
       store_canon(dst + 6, yc.c0);
       store_canon(dst + 9, yc.c1);
-      fp_to_mont(y.c0, yc.c0);
-      fp_to_mont(y.c1, yc.c1);
+      // the chosen root in Montgomery form for the ladder: y's representative made canonical, or
+      // its negation p - y (0 -> 0), instead of converting the canonical bytes back (two multiplies)
+      fp m;
+      fp_reduce_once(y.c0, y.c0);
+      fp_neg_canon(m, y.c0);
+      fp_select(y.c0, keep, y.c0, m);
+      fp_reduce_once(y.c1, y.c1);
+      fp_neg_canon(m, y.c1);
+      fp_select(y.c1, keep, y.c1, m);
 #pragma unroll
       for (int k = 0; k < NL; k++) base[2 * NL + k][threadIdx.x] = y.c0.v[k], base[3 * NL + k][threadIdx.x] = y.c1.v[k];
     }

@@ -325,6 +325,27 @@ KZG_DEV void fp_select(Fe<Tr>& r, bool c, const Fe<Tr>& a, const Fe<Tr>& b) {  /
   for (int i = 0; i < Tr::NL; i++) r.v[i] = c ? a.v[i] : b.v[i];
 }
 
+// r = a / 2 (mod p) for a normalized a (limbs < 2^LB but the top one, top + p's top + 1 < 2^32):
+// a + p if a is odd, then one right shift across the limbs. Normalized out, value (v(a) + 1) / 2.
+// Halving the Montgomery representative halves the element, so this replaces a multiply by
+// Montgomery 1/2 (~490 VALU instructions) with ~4 NL. Bounds: field_bounds_model.half.
+template <class Tr>
+KZG_DEV void fp_half(Fe<Tr>& r, const Fe<Tr>& a) {
+  const uint32_t odd = 0u - (a.v[0] & 1u);
+  Fe<Tr> t;
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < Tr::NL - 1; i++) {
+    const uint32_t s = a.v[i] + (Tr::P[i] & odd) + c;
+    t.v[i] = s & Tr::MASK;
+    c = s >> Tr::LB;
+  }
+  t.v[Tr::NL - 1] = a.v[Tr::NL - 1] + (Tr::P[Tr::NL - 1] & odd) + c;
+#pragma unroll
+  for (int i = 0; i < Tr::NL - 1; i++) r.v[i] = (t.v[i] >> 1) | ((t.v[i + 1] & 1u) << (Tr::LB - 1));
+  r.v[Tr::NL - 1] = t.v[Tr::NL - 1] >> 1;
+}
+
 // normalized a - k (k normalized constant): returns borrow (true if a < k); d = a - k if not
 template <class Tr>
 KZG_DEV bool fp_sub_const_borrow(Fe<Tr>& d, const Fe<Tr>& a, const uint32_t (&k)[Tr::NL]) {
@@ -645,6 +666,24 @@ KZG_DEV void fp_from_f30(fp& r, const f30& z) {
   fp_reduce_once(r, r);
 }
 
+// The exponentiation schedule as one int32 per step, squarings | table index << 8 (index -1: no
+// multiply), plus one padding step. The step loop reads it with a scalar load (s_load_dword) one
+// step ahead: the int8 arrays it replaces can only be read by per-lane global_load_sbyte (SMEM has
+// no byte loads), and each step then waited on a vector-memory round trip (s_waitcnt vmcnt(0))
+// before it could start — 67 waits per exponentiation per wave.
+template <class Tr>
+struct SqrtSchedule {
+  int32_t step[Tr::SQRT_STEPS + 1];
+  constexpr SqrtSchedule() : step{} {
+    for (int s = 0; s < Tr::SQRT_STEPS; s++) step[s] = (Tr::SQRT_STEP_SQ[s] & 0xff) | (Tr::SQRT_STEP_IDX[s] * 256);
+    step[Tr::SQRT_STEPS] = 0;
+  }
+};
+template <class Tr>
+__constant__ constexpr SqrtSchedule<Tr> kSqrtSchedule{};
+KZG_DEV int sched_nsq(int32_t packed) { return __builtin_amdgcn_readfirstlane(packed & 0xff); }
+KZG_DEV int sched_idx(int32_t packed) { return __builtin_amdgcn_readfirstlane(packed >> 8); }
+
 // BLS12-381 r = a^((p-3)/4) on the radix-2^30 core: a (R = 2^392 Montgomery) read as an R30
 // Montgomery integer is the element 4a, so the chain computes (4a)^e and one multiply by
 // POW30_OUT = 2^392 4^-e turns it into a^e in R = 2^392 Montgomery form. Output canonical.
@@ -694,10 +733,11 @@ KZG_DEV void fp_pow_pm3d4_30(fp& r, const fp& a_in) {
   f30 acc;
 #pragma unroll
   for (int k = 0; k < N30; k++) acc.v[k] = (int32_t)tab[k][BlsFp::SQRT_STEP_IDX[0]];
+  int32_t step = kSqrtSchedule<BlsFp>.step[1];
 #pragma unroll 1
   for (int s = 1; s < BlsFp::SQRT_STEPS; s++) {
-    const int nsq = __builtin_amdgcn_readfirstlane(BlsFp::SQRT_STEP_SQ[s]);
-    const int idx = __builtin_amdgcn_readfirstlane(BlsFp::SQRT_STEP_IDX[s]);
+    const int nsq = sched_nsq(step), idx = sched_idx(step);
+    step = kSqrtSchedule<BlsFp>.step[s + 1];  // in flight during this step's squarings
 #pragma unroll 1
     for (int k = 0; k < nsq; k++) f30_sqr(acc, acc);
     if (idx >= 0) {
@@ -742,10 +782,11 @@ KZG_DEV void fp_pow_pm3d4_window(Fe<Tr>& r, const Fe<Tr>& a) {
   Fe<Tr> acc;
 #pragma unroll
   for (int k = 0; k < Tr::NL; k++) acc.v[k] = tab[k][Tr::SQRT_STEP_IDX[0]];
+  int32_t step = kSqrtSchedule<Tr>.step[1];
 #pragma unroll 1
   for (int s = 1; s < Tr::SQRT_STEPS; s++) {
-    const int nsq = __builtin_amdgcn_readfirstlane(Tr::SQRT_STEP_SQ[s]);
-    const int idx = __builtin_amdgcn_readfirstlane(Tr::SQRT_STEP_IDX[s]);
+    const int nsq = sched_nsq(step), idx = sched_idx(step);
+    step = kSqrtSchedule<Tr>.step[s + 1];  // in flight during this step's squarings
 #pragma unroll 1
     for (int k = 0; k < nsq; k++) fp_sqr(acc, acc);
     if (idx >= 0) {

@@ -131,7 +131,8 @@ __global__ void __launch_bounds__(kBlock) k_g1_codec(const uint4* __restrict__ i
     fp yc, nyc;
     fp_from_mont(yc, y);
     fp_neg_canon(nyc, yc);
-    fp_select(yc, fp_lt_canon(yc, nyc) ^ greatest, yc, nyc);
+    const bool keep = fp_lt_canon(yc, nyc) ^ greatest;
+    fp_select(yc, keep, yc, nyc);
     if (st == 0) {
       words w;  // the whole 96-B record in one go: a 48-B half written long before the other costs
       uint32_t lane = threadIdx.x;  // a partial 64-B write per half (PMC: 155 instead of 96 B/point)
@@ -140,7 +141,11 @@ __global__ void __launch_bounds__(kBlock) k_g1_codec(const uint4* __restrict__ i
       for (int k = 0; k < 12; k++) w[k] = qpark[k][lane];
       store_words(dst, w);
       store_canon(dst + 3, yc);
-      fp_to_mont(y, yc);
+      // the chosen root in Montgomery form: y's representative made canonical, or p - y (0 -> 0),
+      // instead of converting the canonical bytes back (a multiply)
+      fp_reduce_once(y, y);
+      fp_neg_canon(t, y);
+      fp_select(y, keep, y, t);
 #pragma unroll
       for (int k = 0; k < NL; k++) base[NL + k][threadIdx.x] = y.v[k];
     }

@@ -670,6 +670,8 @@ static int finish(uint8_t* st, size_t n, uint8_t* out, size_t out_rec, int64_t* 
 }
 
 /* ----------------------------------------------------------------- exported oracle API */
+/* a failed allocation: the library's KZGPOT_E_OUT_OF_MEMORY (include/kzgpot.h) */
+#define ORACLE_E_NOMEM (-108)
 /* threads_decompress: workers for the decompression stage (reference: num_cpus);
  * threads_check: workers for the read_g1/read_g2 + serialize stage (reference: 1). */
 int oracle_g1_decompress(const uint8_t* in, size_t n, uint8_t* out, uint32_t flags, int64_t* first_bad,
@@ -677,6 +679,7 @@ int oracle_g1_decompress(const uint8_t* in, size_t n, uint8_t* out, uint32_t fla
   pthread_once(&init_once, init_consts);
   g1a* pts = (g1a*)calloc(n ? n : 1, sizeof(g1a));
   uint8_t* st = (uint8_t*)calloc(n ? n : 1, 1);
+  if (!pts || !st) return free(pts), free(st), ORACLE_E_NOMEM;
   run_parallel(0, in, out, pts, st, n, flags, threads_decompress);
   run_parallel(2, in, out, pts, st, n, flags, threads_check);
   int r = finish(st, n, out, 96, first_bad, status);
@@ -689,6 +692,7 @@ int oracle_g2_decompress(const uint8_t* in, size_t n, uint8_t* out, uint32_t fla
   pthread_once(&init_once, init_consts);
   g2a* pts = (g2a*)calloc(n ? n : 1, sizeof(g2a));
   uint8_t* st = (uint8_t*)calloc(n ? n : 1, 1);
+  if (!pts || !st) return free(pts), free(st), ORACLE_E_NOMEM;
   run_parallel(1, in, out, pts, st, n, flags, threads_decompress);
   run_parallel(3, in, out, pts, st, n, flags, threads_check);
   int r = finish(st, n, out, 192, first_bad, status);
@@ -699,6 +703,7 @@ int oracle_g2_decompress(const uint8_t* in, size_t n, uint8_t* out, uint32_t fla
 int oracle_g1_transcode(const uint8_t* in, size_t n, uint8_t* out, int64_t* first_bad, uint8_t* status, int threads) {
   pthread_once(&init_once, init_consts);
   uint8_t* st = (uint8_t*)calloc(n ? n : 1, 1);
+  if (!st) return ORACLE_E_NOMEM;
   run_parallel(4, in, out, NULL, st, n, 0, threads);
   int r = finish(st, n, out, 96, first_bad, status);
   free(st);
@@ -707,6 +712,7 @@ int oracle_g1_transcode(const uint8_t* in, size_t n, uint8_t* out, int64_t* firs
 int oracle_g2_transcode(const uint8_t* in, size_t n, uint8_t* out, int64_t* first_bad, uint8_t* status, int threads) {
   pthread_once(&init_once, init_consts);
   uint8_t* st = (uint8_t*)calloc(n ? n : 1, 1);
+  if (!st) return ORACLE_E_NOMEM;
   run_parallel(5, in, out, NULL, st, n, 0, threads);
   int r = finish(st, n, out, 192, first_bad, status);
   free(st);
@@ -738,6 +744,10 @@ int oracle_preprocess(const uint8_t* tr, size_t len, uint64_t n, int fast, uint8
   for (int s = 0; s < 5; s++) {
     size_t rec_in = isg2[s] ? 96 : 48, rec_out = isg2[s] ? 192 : 96;
     outs[s] = (uint8_t*)malloc(cnt[s] * rec_out);
+    if (!outs[s]) {
+      for (int k = 0; k < s; k++) free(outs[k]);
+      return ORACLE_E_NOMEM;
+    }
     uint32_t fl = checked[s] ? 0 : F_NO_SUBGROUP_CHECK;
     int r = isg2[s] ? oracle_g2_decompress(p, cnt[s], outs[s], fl, &fb, NULL, threads, threads)
                     : oracle_g1_decompress(p, cnt[s], outs[s], fl, &fb, NULL, threads, threads);
@@ -931,6 +941,7 @@ static int decompress_all(int g2, const uint8_t* enc, void* pts, size_t len, int
   size_t nt = (len + chunk - 1) / chunk;
   dchunk* cs = (dchunk*)calloc(nt ? nt : 1, sizeof(dchunk));
   pthread_t* tid = (pthread_t*)calloc(nt ? nt : 1, sizeof(pthread_t));
+  if (!cs || !tid) return free(cs), free(tid), -ORACLE_E_NOMEM; /* the caller negates */
   for (size_t t = 0; t < nt; t++) {
     cs[t] = (dchunk){g2, enc, pts, t * chunk, (t + 1) * chunk < len ? (t + 1) * chunk : len, -1, 0};
     if (pthread_create(&tid[t], NULL, decompress_chunk, &cs[t])) decompress_chunk(&cs[t]), tid[t] = 0;
@@ -962,6 +973,10 @@ int oracle_preprocess_pipeline(const char* transcript_path, const char* uncompre
       return -103;
     }
     uint8_t* all = (uint8_t*)malloc(len);
+    if (!all) {
+      close(fd);
+      return ORACLE_E_NOMEM;
+    }
     size_t got = 0;
     while (got < len) {
       ssize_t k = read(fd, all + got, len - got);
@@ -991,13 +1006,15 @@ int oracle_preprocess_pipeline(const char* transcript_path, const char* uncompre
     oracle_blake2b_init(&h);
     breader r = {fd, (uint8_t*)malloc(8192), 8192, 0, 0, &h};
     uint8_t hash64[64];
-    if (br_read_exact(&r, hash64, 64)) ret = -102;
+    if (!r.buf) ret = ORACLE_E_NOMEM;
+    else if (br_read_exact(&r, hash64, 64)) ret = -102;
     for (int s = 0; s < 5 && !ret; s++) {
       const size_t rec = isg2[s] ? 96 : 48;
       uint8_t* enc = (uint8_t*)malloc(cnt[s] * rec);
+      pts[s] = calloc(cnt[s], isg2[s] ? sizeof(g2a) : sizeof(g1a));
+      if (!enc || !pts[s]) ret = ORACLE_E_NOMEM;
       for (size_t i = 0; i < cnt[s] && !ret; i++)
         if (br_read_exact(&r, enc + rec * i, rec)) ret = -102;
-      pts[s] = calloc(cnt[s], isg2[s] ? sizeof(g2a) : sizeof(g1a));
       if (!ret) {
         int e = decompress_all(isg2[s], enc, pts[s], cnt[s], num_cpus);
         if (e) ret = -e;
@@ -1016,14 +1033,15 @@ int oracle_preprocess_pipeline(const char* transcript_path, const char* uncompre
     else {
       bwriter w = {fd, (uint8_t*)malloc(8192), 8192, 0, 0};
       uint8_t b[192];
-      for (int s = 0; s < 5; s++)
+      if (!w.buf) ret = ORACLE_E_NOMEM, w.err = 1;
+      for (int s = 0; s < 5 && w.buf; s++)
         for (size_t i = 0; i < cnt[s]; i++) {
           if (isg2[s]) pairing_g2_uncompressed(b, &((g2a*)pts[s])[i]);
           else pairing_g1_uncompressed(b, &((g1a*)pts[s])[i]);
           bw_write_all(&w, b, isg2[s] ? 192 : 96);
         }
-      bw_flush(&w);
-      if (w.err) ret = -102;
+      if (w.buf) bw_flush(&w);
+      if (w.err && !ret) ret = -102;
       free(w.buf);
       if (close(fd)) ret = -102;
     }
@@ -1040,8 +1058,13 @@ int oracle_preprocess_pipeline(const char* transcript_path, const char* uncompre
     else {
       breader r = {fd, (uint8_t*)malloc(1 << 20), 1 << 20, 0, 0, NULL};
       uint8_t b[192];
+      if (!r.buf) ret = ORACLE_E_NOMEM;
       for (int s = 0; s < nload && !ret; s++) {
         ark[s] = calloc(cnt[s], isg2[s] ? sizeof(g2a) : sizeof(g1a));
+        if (!ark[s]) {
+          ret = ORACLE_E_NOMEM;
+          break;
+        }
         for (size_t i = 0; i < cnt[s] && !ret; i++) {
           if (br_read_exact(&r, b, isg2[s] ? 192 : 96)) {
             ret = -102;

@@ -213,6 +213,16 @@ def norm(a, name="norm"):
     return normalized(a.val, name)
 
 
+def half(a, name="half"):
+    """fp_half: a normalized (limbs below the top < 2^28); + p if odd (the top limb absorbs the
+    carry), then one right shift across the limbs: normalized, value (v + 1) / 2."""
+    if any(l > LM for l in a.limbs[: NL - 1]):
+        raise BoundError(f"{name}: input not normalized {a!r}")
+    if a.limbs[NL - 1] + P_L[NL - 1] + 1 >= 1 << 32:
+        raise BoundError(f"{name}: top limb + p may overflow {a!r}")
+    return normalized((a.val + 1) / 2 * UP, name)
+
+
 def canon_ok(a, name="canon"):
     """fp_canon / fp_is_zero precondition: limbs < 2^32 - 16 (fp_norm), value < 256 p."""
     if max(a.limbs) >= (1 << 32) - 16 or a.val >= 256:

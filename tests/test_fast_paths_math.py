@@ -79,34 +79,70 @@ def test_fast_equals_ref_on_adversarial_points():
         assert g2_fast(pt) == g2_ref(pt)
 
 
-def fp2_sqrt_norm(a):
-    """Restatement of fp2_sqrt (codec_kernels.hip)."""
+def _half(v):
+    """fp_half: + p if odd, then >> 1 (the element v / 2)."""
+    return (v + (P if v & 1 else 0)) >> 1
+
+
+def fp2_sqrt_norm(a, accept_by_y2=False):
+    """Restatement of fp2_sqrt (codec_kernels.hip): accepted iff gam^2 == N (accept_by_y2: the
+    earlier y^2 == a test instead, for the equivalence check below)."""
     a0, a1 = a
     nrm = (a0 * a0 + a1 * a1) % P
     gam = pow(nrm, (P - 3) // 4, P) * nrm % P
-    ok1 = gam * gam % P == nrm
-    inv2 = pow(2, P - 2, P)
-    d = (a0 + gam) * inv2 % P
+    square = gam * gam % P == nrm
+    d = _half((a0 + gam) % P)
     if d == 0:
         d = a0
     t = pow(d, (P - 3) // 4, P)
     s = t * d % P
-    h = a1 * t % P * inv2 % P
+    h = _half(a1) * t % P
     y = (s, h) if s * s % P == d else ((-h) % P, s)
-    return y if ok1 and O.fp2_sqr(y) == (a0 % P, a1 % P) else None
+    ok = O.fp2_sqr(y) == (a0 % P, a1 % P) if accept_by_y2 else square
+    return y if ok else None
+
+
+def _fp2_sqrt_cases(rng):
+    cases = [(0, 0), (1, 0), (P - 1, 0), (0, 1), (0, P - 1), (4, 0), (5, 0), (0, 7), (2, 0), (P - 2, 0)]
+    cases += [(rng.randrange(P), rng.randrange(P)) for _ in range(60)]
+    cases += [(rng.randrange(P), 0) for _ in range(10)] + [(0, rng.randrange(P)) for _ in range(10)]
+    # squares (a0 + gam = 0 happens for a = (-c^2, 0): N = c^4, gam = c^2 or -c^2)
+    for _ in range(10):
+        c = rng.randrange(1, P)
+        cases += [((-c * c) % P, 0), (c * c % P, 0), O.fp2_sqr((rng.randrange(P), rng.randrange(P)))]
+    return cases
 
 
 def test_fp2_sqrt_equivalence():
     rng = random.Random(11)
-    cases = [(0, 0), (1, 0), (P - 1, 0), (0, 1), (0, P - 1), (4, 0), (5, 0), (0, 7)]
-    cases += [(rng.randrange(P), rng.randrange(P)) for _ in range(60)]
-    cases += [(rng.randrange(P), 0) for _ in range(10)] + [(0, rng.randrange(P)) for _ in range(10)]
-    for a in cases:
+    for a in _fp2_sqrt_cases(rng):
         ref = O.fq2_sqrt(a)
         got = fp2_sqrt_norm(a)
         assert (ref is None) == (got is None), a
         if ref is not None:
             assert got in (ref, O.fp2_neg(ref))
+
+
+def test_fp2_sqrt_norm_test_equals_y2_test():
+    """The kernel accepts a iff gam^2 == N; the y^2 == a test it replaced decides the same for
+    every a (codec_kernels.hip fp2_sqrt's derivation), including d = a0 + gam = 0 and a1 = 0."""
+    rng = random.Random(12)
+    cases = _fp2_sqrt_cases(rng)
+    for a in cases:
+        assert (fp2_sqrt_norm(a) is None) == (fp2_sqrt_norm(a, accept_by_y2=True) is None), a
+        got = fp2_sqrt_norm(a)
+        if got is not None:
+            assert O.fp2_sqr(got) == (a[0] % P, a[1] % P), a
+    hits = sum(1 for a in cases if (a[0] + pow((a[0] ** 2 + a[1] ** 2) % P, (P + 1) // 4, P)) % P == 0)
+    assert hits > 0  # the d = 0 fallback is exercised
+
+
+def test_half_is_division_by_two():
+    rng = random.Random(13)
+    inv2 = pow(2, P - 2, P)
+    for v in [0, 1, 2, P - 1, P, P + 1, 2 * P - 1, 3 * P - 2] + [rng.randrange(3 * P) for _ in range(200)]:
+        h = _half(v)
+        assert h % P == v * inv2 % P and h <= (v + P) // 2
 
 
 @pytest.mark.parametrize("hdr,nl,lb", [("bls12_381_consts.hpp", 14, 28), ("bn254_consts.hpp", 9, 29)])

@@ -130,3 +130,28 @@ def test_codec_stall_summary_ratios(tmp_path):
     assert abs(k["simd_cycles_per_valu"] - 31.25 * 128 / 980) < 1e-12
     assert abs(k["valu_issue_frac_at_4_cycles"] - 4 * 980 / (31.25 * 128)) < 1e-12
     assert k["valu_exec_utilisation"] == 1.0 and k["lds_bank_conflict_per_lds_inst"] == 0.5
+
+
+def test_isa_sites_finds_the_hot_loops():
+    """tools/isa_sites.py (the per-site SALU / branch attribution committed under profiles/) on the
+    built library: it must find each codec's square-root loops (a radix-2^30 squaring is 260
+    v_mad_i64_i32; G2 inlines two exponentiations) and the ladder doubling loop, and the loops it
+    attributes must hold most of the per-wave VALU stream (the schedule: 67 steps, 375 squarings)."""
+    from conftest import PKG
+
+    lib = os.path.join(PKG, "build", "libkzgpot.so")
+    if not os.path.exists(lib):
+        subprocess.run(["make", "-C", PKG, "-j", "8"], check=True)
+    out = subprocess.run([sys.executable, os.path.join(TOOLS, "isa_sites.py"), "--lib", lib], capture_output=True,
+                         text=True, check=True).stdout
+    res = json.loads(out)["kernels"]
+    for name, copies, ladder_trips in (("k_g1_codec", 1, 124), ("k_g2_codec", 2, 62)):
+        sites = res[name]["loop_sites"]
+        sq = [s for s in sites if s["site"].startswith("sqrt: f30 squaring loop (window")]
+        win = [s for s in sites if s["site"].startswith("sqrt: window step")]
+        lad = [s for s in sites if s["site"].startswith("ladder")]
+        assert len(sq) == copies and len(win) == copies and len(lad) == 1, (name, [s["site"] for s in sites])
+        assert all(s["trips_per_wave"] == 375 for s in sq) and all(s["trips_per_wave"] == 67 for s in win)
+        assert lad[0]["trips_per_wave"] == ladder_trips
+        # the loops carry the bulk of the VALU stream (PMC: 601 K / 947 K per wave)
+        assert res[name]["loops_per_wave"]["valu"] > (480_000 if name == "k_g1_codec" else 800_000)

@@ -19,6 +19,9 @@
 #   loader_stalls tools/pmc_loader_stalls.sh
 #   loader_ceiling tools/microbench/bin/loader_ceiling (the loader's pattern variants, TB/s)
 #   gloo2         bench.py --gpus 2 --dist-backend gloo (the N > 1 launch path on one GPU)
+#   gloo8         bench.py --gpus 8 --dist-backend gloo at reduced sizes: the driver's world-8 control
+#                 flow (8 spawned ranks, the rendezvous-store wait, rank 0's e2e at 8 shards, the exit
+#                 code) on the one GPU of the box
 #   gather1       bench.py --gather-at-1 (the library's RCCL path at one rank)
 #   port          tests/test_gpu_oracle_port.py alone (every point vs the GPU port of the oracle)
 #   campaign      tools/random_campaign.py for 9 minutes (SEED0=... for fresh seeds)
@@ -55,6 +58,10 @@ for step in "$@"; do
     loader_stalls) timeout -k 10 400 bash tools/pmc_loader_stalls.sh ;;
     gloo2) timeout -k 10 400 python bench.py --gpus 2 --dist-backend gloo --g1-log2 24 --steps 2 --warmup 1 \
              --bn254-log2 0 --no-cpu-baseline > ${o}_bench_gloo2.json 2> ${o}_bench_gloo2.err ;;
+    gloo8) t0=$(date +%s%N); timeout -k 10 600 python bench.py --gpus 8 --dist-backend gloo --g1-log2 23 --g2-log2 13 \
+             --steps 2 --warmup 1 --bn254-log2 23 --e2e-log2 18 --no-cpu-baseline > ${o}_bench_gloo8.json \
+             2> ${o}_bench_gloo8.err; rc=$?; echo "wall_ms $(( ($(date +%s%N) - t0) / 1000000 )) rc $rc" \
+             > ${o}_bench_gloo8.wall; (exit $rc) ;;
     gather1) timeout -k 10 400 python bench.py --gather-at-1 --steps 2 --no-cpu-baseline --no-next-rows \
                > ${o}_bench_gather_at_1.json 2> ${o}_bench_gather_at_1.err ;;
     port) timeout -k 10 1000 python -u -m pytest tests/test_gpu_oracle_port.py -x -v --timeout 900 \

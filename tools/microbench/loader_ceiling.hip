@@ -306,6 +306,27 @@ int main(int argc, char** argv) {
       CHECK(hipDeviceSynchronize());
       CHECK(hipMemcpy(got, out, ob, hipMemcpyDeviceToHost));
       printf("verify %-14s %s\n", name, memcmp(want, got, nb) == 0 ? "equal" : "DIFFERENT");
+      // where they differ: the first differing byte's record and field, and
+      // how many records differ
+      const size_t rec = nb == n * 104 ? 104 : 200;
+      size_t first = nb, nrec = 0;
+      for (size_t r = 0; r < nb / rec; r++) {
+        if (memcmp(want + r * rec, got + r * rec, rec) == 0) continue;
+        if (!nrec)
+          for (size_t b = 0; b < rec; b++)
+            if (want[r * rec + b] != got[r * rec + b]) {
+              first = r * rec + b;
+              break;
+            }
+        nrec++;
+      }
+      if (nrec) {
+        const size_t r = first / rec, b = first % rec;
+        printf("  first difference: record %zu (block %zu of the variant's grid), byte %zu of %zu (%s), "
+               "product %02x variant %02x; %zu of %zu records differ\n",
+               r, r / (rec == 104 ? 128 : 32), b, rec, b < rec - 8 ? "coordinate" : "infinity flag / padding",
+               want[first], got[first], nrec, nb / rec);
+      }
     };
     cmp("DIN 128 (G1)", n * 104, [&] { CHECK(kzgpot::launch_load(false, in, out, n, key, nullptr, 0)); }, [&] {
       hipLaunchKernelGGL((kzgpot::k_load_din<2, 128, true, 1>), dim3((unsigned)(n / 128)), dim3(256), 0, 0, in, out,
