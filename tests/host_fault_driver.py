@@ -8,6 +8,9 @@ shows up as the child's exit status instead of killing pytest.
   host_fault_driver.py cpu   — the paths before any device work (runs without a GPU)
   host_fault_driver.py gpu   — every thread start of a 3-shard file call in turn (needs a GPU)
 
+It checks its own results (problems(), the test's requirements) and exits 3 on a violation, so
+tools/asan_gpu_tests.sh can run it as a top-level process under the host-ASan build.
+
 The transcript is the config-1 fixture (tests/golden/transcript_n1024.bin, N = 2^10)."""
 import ctypes
 import glob
@@ -102,8 +105,46 @@ def main():
     for p in glob.glob(os.path.join(work, "*")):
         os.unlink(p)
     os.rmdir(work)
+    res["problems"] = problems(what, res)
     print(json.dumps(res))
+    return 3 if res["problems"] else 0
+
+
+E_DEVICE, E_OOM = -101, -108
+
+
+def problems(what, res):
+    """What tests/test_host_faults.py requires of a run, as a list of violations (empty = pass)."""
+    bad = []
+    if what == "cpu":
+        if len(res["cases"]) != 5:
+            bad.append("expected 5 cases")
+        for c in res["cases"]:
+            if c["ret"] != E_OOM or c["status"] != "OutOfMemory":
+                bad.append(f"{c['name']}: returned {c['ret']}")
+            if c["tmp_left"] or c["out_exists"]:
+                bad.append(f"{c['name']}: left {c['tmp_left']} / output {c['out_exists']}")
+            if c["bad_section"] != -1 or c["bad_index"] != -1:
+                bad.append(f"{c['name']}: bad_section / bad_index set")
+        if res.get("no_fault_no_gpu") not in (0, E_DEVICE):
+            bad.append(f"no fault: returned {res.get('no_fault_no_gpu')}")
+    else:
+        if len(res["cases"]) != 2 * 20:
+            bad.append("expected 40 cases")
+        for c in res["cases"]:
+            tag = f"mode {c['mode']} skip {c['skip']}"
+            if c["tmp_left"]:
+                bad.append(f"{tag}: left {c['tmp_left']}")
+            if c["skip"] < 19:
+                if c["ret"] != E_OOM or c["out_exists"] or c["bad_section"] != -1 or c["bad_index"] != -1:
+                    bad.append(f"{tag}: returned {c['ret']}, output {c['out_exists']}")
+            elif not (c["ret"] == 0 and c["file_ok"] and c["output_digest_ok"]):
+                bad.append(f"{tag}: the release-only fault must still write the reference file ({c['ret']})")
+        for a in res.get("after", []):
+            if not (a["ret"] == 0 and a["output_digest_ok"] and not a["tmp_left"]):
+                bad.append(f"mode {a['mode']}: the clean call afterwards failed ({a['ret']})")
+    return bad
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

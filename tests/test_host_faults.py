@@ -29,9 +29,12 @@ def _run(what, timeout=240):
     env = dict(os.environ)
     env.setdefault("KZGPOT_LIB", TEST_LIB)
     p = subprocess.run([sys.executable, DRIVER, what], capture_output=True, text=True, timeout=timeout, env=env)
-    # an exception across the C ABI would have ended the child with SIGABRT (-6)
-    assert p.returncode == 0, (p.returncode, p.stderr[-3000:])
-    return json.loads(p.stdout.strip().splitlines()[-1])
+    # an exception across the C ABI would have ended the child with SIGABRT (-6); 3 = the driver's
+    # own check of the results failed (host_fault_driver.problems)
+    assert p.returncode in (0, 3), (p.returncode, p.stderr[-3000:])
+    res = json.loads(p.stdout.strip().splitlines()[-1])
+    assert not res["problems"], res["problems"]
+    return res
 
 
 def test_status_name_out_of_memory(kzgpot_mod):
@@ -40,16 +43,11 @@ def test_status_name_out_of_memory(kzgpot_mod):
 
 def test_host_faults_before_device_work():
     """Runs without a GPU: the transcript hasher, the two file-buffer mappings and the reader
-    thread, each failing in turn, return -108 with no temporary file and no output."""
+    thread, each failing in turn, return -108 with no temporary file and no output
+    (host_fault_driver.problems holds the requirements); with no fault, a machine without a GPU
+    is a device error (the hasher joined first)."""
     res = _run("cpu")
-    assert len(res["cases"]) == 5
-    for c in res["cases"]:
-        assert c["ret"] == E_OOM and c["status"] == "OutOfMemory", c
-        assert c["tmp_left"] == [] and not c["out_exists"], c
-        assert c["bad_section"] == -1 and c["bad_index"] == -1, c
-    # and with no fault, a machine without a GPU is a device error (the hasher joined first)
-    if res.get("no_fault_no_gpu") != 0:
-        assert res["no_fault_no_gpu"] == E_DEVICE
+    assert [c["ret"] for c in res["cases"]] == [E_OOM] * 5
 
 
 @pytest.fixture(scope="module")
@@ -68,13 +66,4 @@ def test_every_thread_start_failing_returns_out_of_memory(capi):
     only the release fails, the call succeeds (the buffers go on the calling thread) and the file
     is the reference file. Afterwards a clean call still writes it."""
     res = _run("gpu", timeout=600)
-    for c in res["cases"]:
-        assert c["tmp_left"] == [], c
-        if c["skip"] < 19:
-            assert c["ret"] == E_OOM and not c["out_exists"], c
-            assert c["bad_section"] == -1 and c["bad_index"] == -1, c
-        else:
-            assert c["ret"] == 0 and c["file_ok"] and c["output_digest_ok"], c
-    assert len(res["cases"]) == 2 * 20
-    for a in res["after"]:
-        assert a["ret"] == 0 and a["output_digest_ok"] and a["tmp_left"] == [], a
+    assert sum(c["ret"] == E_OOM for c in res["cases"]) == 2 * 19
