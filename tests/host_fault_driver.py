@@ -33,12 +33,17 @@ def main():
     lib = ctypes.CDLL(LIB)
     lib.kzgpot_test_inject_host_fault.argtypes = [ctypes.c_int, ctypes.c_long]
     lib.kzgpot_status_name.restype = ctypes.c_char_p
+    # initialise the HIP runtime on this thread first, as every other test process has by the time
+    # it reaches the file pipeline: under the host-ASan runtime (tools/asan_gpu_tests.sh) a runtime
+    # first initialised beside the library's transcript-hasher thread aborted in HSA's pool
+    # allocation ("AddressSanitizer: out of memory", profiles/r06a_asan_fault_child.txt)
+    res_devices = lib.kzgpot_device_count()
     meta = json.load(open(os.path.join(GOLDEN, "transcript_n1024.json")))
     src = os.path.join(GOLDEN, "transcript_n1024.bin")
     tr = open(src, "rb").read()
     work = tempfile.mkdtemp(prefix="kzgpot_fault_")
     out_path = os.path.join(work, "kzg_setup")
-    res = {"lib": LIB, "cases": []}
+    res = {"lib": LIB, "devices": res_devices, "cases": []}
 
     def leftovers():
         return sorted(os.path.basename(p) for p in glob.glob(out_path + ".kzgpot-tmp-*"))

@@ -78,6 +78,12 @@ def summarise(c):
             ("branch", "SQ_INSTS_BRANCH"), ("salu_cycles", "SQ_INST_CYCLES_SALU"))},
         "lds_bank_conflict_per_lds_inst": c.get("SQ_LDS_BANK_CONFLICT", 0) / max(1, c.get("SQ_INSTS_LDS", 0)),
         "lds_in_flight_per_wave": c.get("SQ_INST_LEVEL_LDS", 0) / wc,
+        # the instruction-fetch pass (round 6): SQC instruction-cache misses per wave and per
+        # 1,000 VALU instructions, and the miss rate of the instruction fetches
+        **({"icache_misses_per_wave": c["SQC_ICACHE_MISSES"] / waves,
+            "icache_misses_per_kvalu": 1000 * c["SQC_ICACHE_MISSES"] / valu,
+            "icache_miss_rate": c["SQC_ICACHE_MISSES"] / max(1, c.get("SQC_ICACHE_HITS", 0) + c["SQC_ICACHE_MISSES"]),
+            "ifetch_per_valu": c.get("SQ_IFETCH", 0) / valu} if "SQC_ICACHE_MISSES" in c else {}),
         "raw": dict(c),
     }
 
