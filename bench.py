@@ -614,6 +614,18 @@ def loader_row(kind, src, out, key, m, what):
             "all_accepted": D.read_key(key) == KD.NO_BAD}
 
 
+def g2_vs_g1(g1v, g2v, g1_ms, g2_ms):
+    """Clock-free efficiency of the G2 codec relative to the G1 codec launched alternately with it:
+    (G2 : G1 time predicted by their VALU counts x opcode-mix cycles) / (measured G2 : G1 time).
+    1.0 = G2 converts its instructions into time exactly as well as G1 does."""
+    try:
+        model = (g2v["valu_instr_per_point"] * g2v["avg_simd_cycles_per_instr"]) / \
+                (g1v["valu_instr_per_point"] * g1v["avg_simd_cycles_per_instr"])
+    except (TypeError, KeyError):
+        return None
+    return {"model_time_ratio": model, "measured_time_ratio": g2_ms / g1_ms, "efficiency": model / (g2_ms / g1_ms)}
+
+
 def transcode_row(kind, pin, out, key, want, n):
     """SURVEY §8f row 3 (the reference's read_g1 / read_g2 loop, preprocess-kgz.rs:140-153,
     src/lib.rs:41-80): one event-timed launch of the transcode kernel over n pairing-uncompressed
@@ -1164,38 +1176,39 @@ def main():
         k3 = torch.empty(2, dtype=torch.int64, device=dev)
         D.codec_dev("g1_decompress", c31, o31, k3[0:1], g1_flags)
         D.codec_dev("g2_decompress", c32, o32, k3[1:2], g1_flags)
-        # one launch is ~17 / ~27 ms: three of each, each event-timed, and each group of three
-        # bracketed by the shader-clock probe, so that each group is priced at the clock the GPU ran
-        # during THAT group (the G2 fraction used the headline's clock)
+        # three pairs of launches (~17 + ~27 ms each), each launch event-timed, G1 and G2 alternating
+        # so that both run under the same clock, which the shader-clock probe measures over the
+        # whole interleaved region; the G2 : G1 time ratio against their VALU models' ratio is a
+        # clock-free measure of how far G2 sits below G1's efficiency
         reps3 = 3
-        group_clock = {}
-        per = {}
-        for kind, cin, cout, kk in (("g1", c31, o31, k3[0:1]), ("g2", c32, o32, k3[1:2])):
-            ce = [torch.cuda.Event(enable_timing=True) for _ in range(reps3 + 1)]
-            p0 = D.clock_probe(dev)
-            ce[0].record()
-            for r in range(reps3):
-                D.codec_dev(f"{kind}_decompress", cin, cout, kk, g1_flags)
-                ce[r + 1].record()
-            p1 = D.clock_probe(dev)
-            torch.cuda.synchronize()
-            per[kind] = [ce[r].elapsed_time(ce[r + 1]) for r in range(reps3)]
-            group_clock[kind] = D.clock_mhz(p0, p1)
+        ce = [torch.cuda.Event(enable_timing=True) for _ in range(2 * reps3 + 1)]
+        p0 = D.clock_probe(dev)
+        ce[0].record()
+        for r in range(reps3):
+            D.codec_dev("g1_decompress", c31, o31, k3[0:1], g1_flags)
+            ce[2 * r + 1].record()
+            D.codec_dev("g2_decompress", c32, o32, k3[1:2], g1_flags)
+            ce[2 * r + 2].record()
+        p1 = D.clock_probe(dev)
+        torch.cuda.synchronize()
+        per = {"g1": [ce[2 * r].elapsed_time(ce[2 * r + 1]) for r in range(reps3)],
+               "g2": [ce[2 * r + 1].elapsed_time(ce[2 * r + 2]) for r in range(reps3)]}
+        c3_clock = D.clock_mhz(p0, p1)
         g1s, g2s = per["g1"], per["g2"]
         g1c, g2c = sum(g1s) / reps3, sum(g2s) / reps3
+        g1v = valu_roofline(load_json("pmc_traffic.json"), load_json("r02_valu_mix.json"),
+                            ["k_g1_decompress", "k_g1_check"] if args.split_phases else ["k_g1_codec"], n3, g1c, c3_clock)
+        g2v = valu_roofline(load_json("pmc_traffic.json"), load_json("r02_valu_mix.json"),
+                            ["k_g2_decompress", "k_g2_check"] if args.split_phases else ["k_g2_codec"], n3, g2c, c3_clock)
         next_rows["config3_g1_g2_2e20"] = {
             "workload": "config 3: 2^20 G1 + 2^20 G2 compressed -> ark uncompressed, subgroup-checked, 1 GPU",
             "g1_ms": g1c, "g2_ms": g2c, "reps": reps3, "g1_ms_each": g1s, "g2_ms_each": g2s,
             "points_per_s": 2 * n3 / ((g1c + g2c) * 1e-3),
             "g2_ns_per_point": g2c * 1e6 / n3,
-            "clock_mhz_during": {k: (None if v is None else v["mean"]) for k, v in group_clock.items()},
+            "clock_mhz": None if c3_clock is None else c3_clock["mean"],
             "headline_clock_mhz": None if clock is None else clock["mean"],
-            "g1_valu": valu_roofline(load_json("pmc_traffic.json"), load_json("r02_valu_mix.json"),
-                                     ["k_g1_decompress", "k_g1_check"] if args.split_phases else ["k_g1_codec"],
-                                     n3, g1c, group_clock.get("g1")),
-            "g2_valu": valu_roofline(load_json("pmc_traffic.json"), load_json("r02_valu_mix.json"),
-                                     ["k_g2_decompress", "k_g2_check"] if args.split_phases else ["k_g2_codec"],
-                                     n3, g2c, group_clock.get("g2")),
+            "g1_valu": g1v, "g2_valu": g2v,
+            "g2_efficiency_vs_g1": g2_vs_g1(g1v, g2v, g1c, g2c),
             "verified_bit_exact": bool(D.read_key(k3[0:1]) == KD.NO_BAD and D.read_key(k3[1:2]) == KD.NO_BAD
                                        and torch.equal(o31, x31) and torch.equal(o32, x32))}
         # row 3, G2 (the read_g2 loop, the reference's HOT LOOP 2 for τG2): config 3's 2^20 ark G2
