@@ -33,11 +33,17 @@ def main():
     lib = ctypes.CDLL(LIB)
     lib.kzgpot_test_inject_host_fault.argtypes = [ctypes.c_int, ctypes.c_long]
     lib.kzgpot_status_name.restype = ctypes.c_char_p
-    # initialise the HIP runtime on this thread first, as every other test process has by the time
-    # it reaches the file pipeline: under the host-ASan runtime (tools/asan_gpu_tests.sh) a runtime
-    # first initialised beside the library's transcript-hasher thread aborted in HSA's pool
-    # allocation ("AddressSanitizer: out of memory", profiles/r06a_asan_fault_child.txt)
+    # put the GPU to work on this (main) thread first, as every other test process has by the time
+    # it reaches the file pipeline: under the host-ASan runtime (tools/asan_gpu_tests.sh) a process
+    # whose first device allocation came from one of the library's shard threads aborted in HSA's
+    # pool allocation ("AddressSanitizer: out of memory", profiles/r06a_asan_fault_child.txt); one
+    # generator point decoded here (the G1 generator's published encoding) avoids that
     res_devices = lib.kzgpot_device_count()
+    if res_devices > 0:
+        gen = bytes.fromhex("97f1d3a73197d7942695638c4fa9ac0fc3688c4f9774b905a14e3a3f171bac586c55e83ff97a1aeffb3af00adb22c6bb")
+        o96, fb = ctypes.create_string_buffer(96), ctypes.c_int64(0)
+        if lib.kzgpot_g1_decompress(gen, ctypes.c_size_t(1), o96, 0, ctypes.byref(fb)) != 0:
+            raise SystemExit("the G1 generator did not decode")
     meta = json.load(open(os.path.join(GOLDEN, "transcript_n1024.json")))
     src = os.path.join(GOLDEN, "transcript_n1024.bin")
     tr = open(src, "rb").read()
