@@ -30,7 +30,7 @@ MODE_KZG, MODE_FASTKZG = 0, 1
 
 def main():
     what = sys.argv[1]
-    lib = ctypes.CDLL(LIB)
+    lib = ctypes.CDLL(LIB, mode=ctypes.RTLD_GLOBAL)  # as kzgpot._lib.load() binds it
     lib.kzgpot_test_inject_host_fault.argtypes = [ctypes.c_int, ctypes.c_long]
     lib.kzgpot_status_name.restype = ctypes.c_char_p
     # put the GPU to work on this (main) thread first, as every other test process has by the time
