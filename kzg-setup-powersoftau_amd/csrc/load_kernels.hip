@@ -154,6 +154,62 @@ __global__ void __launch_bounds__(PTS * NC / CPL) k_load(const uint4* __restrict
   }
 }
 
+// G1 with DIRECT input: each lane reads its 48-B coordinate straight from HBM (three 16-B loads
+// at the record stride, through the caches: the three loads of a wave cover its 3 KB of records
+// together) and only the output goes through the LDS slab, so the block has one barrier instead
+// of two. Same bytes as k_load<2, 128, true, 1> (tools/microbench/loader_ceiling.hip verifies
+// them). Measured against the staged kernel on three boxes in round 6: 5.63 / 5.81 / 5.63 TB/s
+// against 5.38 / 5.55 / 5.40 (profiles/r06b, r06d, r06e_loader_ceiling.txt, "DIN plain 128");
+// one round-5 box had it 2 % slower (r05i). With nontemporal loads it is slower everywhere: the
+// three loads of a lane pair's record are the cache lines the streaming hint would evict.
+template <int PTS>
+__global__ void __launch_bounds__(PTS * 2) k_load_g1_direct(const uint4* __restrict__ in, uint4* __restrict__ out,
+                                                            uint64_t n, unsigned long long* __restrict__ first_bad,
+                                                            uint8_t* __restrict__ status) {
+  constexpr int BLK = PTS * 2, RIN = 96, ROUT = 104;  // a point is a lane pair: x, then y with the flags
+  static_assert((PTS * ROUT) % 16 == 0, "slab alignment");
+  __shared__ uint4 slab[PTS * ROUT / 16];
+  const uint64_t base = (uint64_t)blockIdx.x * PTS;
+  const int cnt = (int)((n - base) < (uint64_t)PTS ? (n - base) : (uint64_t)PTS);
+  const int t = threadIdx.x, pt = t / 2, h = t % 2;
+  int st = 0;
+  bool finf = false;
+  words res;
+  if (pt < cnt) {
+    words c;
+    load_le(c, in + (base + pt) * (RIN / 16) + 3 * h);
+    const uint32_t yb = c[11] >> 24;
+    finf = h == 1 && (yb & 0x40u);
+    if (h == 1) {
+      c[11] &= 0x3fffffffu;
+      if ((yb & 0x80u) && finf) st = 6;  // both SWFlags: UnexpectedFlags, before y's range check
+    }
+    if (!st && words_geq_p(c)) st = 3;
+    words_to_ark_mont(res, c);
+  }
+  // the point's status: x's lane first (ark reads x before y's flags), else y's
+  const int other = __shfl_xor(st, 1);
+  st = h == 0 ? (st ? st : other) : (other ? other : st);
+  if (pt < cnt) {
+    uint2* dst = (uint2*)slab + pt * (ROUT / 8) + 6 * h;
+#pragma unroll
+    for (int j = 0; j < 6; j++) dst[j] = st ? make_uint2(0, 0) : make_uint2(res[2 * j], res[2 * j + 1]);
+    if (h == 1) {
+      dst[6] = make_uint2((!st && finf) ? 1u : 0u, 0u);
+      report(base + pt, st, first_bad, status);
+    }
+  }
+  __syncthreads();
+  if (cnt == PTS) {
+    uint4* dst = (uint4*)((uint8_t*)out + base * ROUT);
+    for (int k = t; k < PTS * ROUT / 16; k += BLK) st_stream(dst + k, slab[k]);
+  } else {  // ragged tail block: the slab ends on an 8-B boundary
+    uint2* dst = (uint2*)out + base * (ROUT / 8);
+    const uint2* s2 = (const uint2*)slab;
+    for (int k = t; k < cnt * (ROUT / 8); k += BLK) dst[k] = s2[k];
+  }
+}
+
 hipError_t launch_load(bool g2, const void* d_in, void* d_out, uint64_t n, unsigned long long* d_first_bad,
                        uint8_t* d_status, hipStream_t stream) {
   if (n == 0) return hipSuccess;
@@ -165,8 +221,8 @@ hipError_t launch_load(bool g2, const void* d_in, void* d_out, uint64_t n, unsig
     hipLaunchKernelGGL((k_load<4, P>), dim3((unsigned)((n + P - 1) / P)), dim3(P * 2), 0, stream, (const uint4*)d_in,
                        (uint4*)d_out, n, d_first_bad, d_status);
   } else {
-    constexpr int P = 128;  // one coordinate per lane: 256 lanes, 13.3 KB of slab
-    hipLaunchKernelGGL((k_load<2, P, true, 1>), dim3((unsigned)((n + P - 1) / P)), dim3(P * 2), 0, stream,
+    constexpr int P = 128;  // one coordinate per lane: 256 lanes, 13.3 KB of output slab
+    hipLaunchKernelGGL((k_load_g1_direct<P>), dim3((unsigned)((n + P - 1) / P)), dim3(P * 2), 0, stream,
                        (const uint4*)d_in, (uint4*)d_out, n, d_first_bad, d_status);
   }
   return hipGetLastError();
