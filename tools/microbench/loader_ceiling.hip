@@ -9,7 +9,8 @@
 //   slab_nt       : slab with nontemporal loads and stores
 //   slab_glds_nt  : slab whose input sweep is global_load_lds_dwordx4 (LDS-DMA, no VGPR round trip)
 //                   + nontemporal stores
-//   k_load        : the product kernel (kzgpot::launch_load, G1), for the same bytes
+//   product G1    : the product kernel (kzgpot::launch_load, G1: k_load_g1_direct since round 6),
+//                   for the same bytes; "k_load 1c/l 128" is the round-5 product (staged in and out)
 //   k_load_pipe   : an experiment: a resident grid (x f/4 of the occupancy-limited block count)
 //                   walks the slabs grid-stride, prefetching the next slab's input into registers
 //                   while it converts and stores the current one. Slower than letting the hardware
@@ -117,11 +118,13 @@ __global__ void __launch_bounds__(PTS * NC / CPL) k_load_pipe(const uint4* __res
     __syncthreads();  // the slab is read out before the next slab's input overwrites it
   }
 }
-// EXPERIMENT (not in the product; measured slower, profiles/r05i_loader_ceiling.txt): k_load with
-// DIRECT input — each lane reads its own coordinates straight from global memory (48-B pieces at
-// the record stride) instead of from a staged input slab; the slab stages only the output, and
-// the block's first barrier goes away. G1: 5.26 TB/s (5.50 without the nontemporal hint) against
-// 5.61 for the staged product kernel; G2: 3.70 against 5.62.
+// k_load with DIRECT input — each lane reads its own coordinates straight from global memory (48-B
+// pieces at the record stride) instead of from a staged input slab; the slab stages only the
+// output, and the block's first barrier goes away. G2 (two coordinates per lane): 3.70-3.83 TB/s
+// against 5.56-5.62 for the staged kernel (r05i, r06*). G1 with plain loads: faster than the staged
+// kernel on three of four round-6 boxes (r06b/d/e: 5.63-5.81 against 5.38-5.55 TB/s, equal on
+// r06f), slower on r05i's (5.48 / 5.61) — the product G1 loader since round 6 (k_load_g1_direct in
+// load_kernels.hip); with nontemporal loads slower everywhere.
 template <int NC, int PTS, bool NT, int CPL>
 __global__ void __launch_bounds__(PTS * NC / CPL) k_load_din(const uint4* __restrict__ in, uint4* __restrict__ out,
                                                              uint64_t n, unsigned long long* __restrict__ first_bad,
@@ -328,6 +331,10 @@ int main(int argc, char** argv) {
                want[first], got[first], nrec, nb / rec);
       }
     };
+    cmp("staged (G1)", n * 104, [&] { CHECK(kzgpot::launch_load(false, in, out, n, key, nullptr, 0)); }, [&] {
+      hipLaunchKernelGGL((kzgpot::k_load<2, 128, true, 1>), dim3((unsigned)(n / 128)), dim3(256), 0, 0, in, out, n,
+                         key, nullptr);
+    });
     cmp("DIN 128 (G1)", n * 104, [&] { CHECK(kzgpot::launch_load(false, in, out, n, key, nullptr, 0)); }, [&] {
       hipLaunchKernelGGL((kzgpot::k_load_din<2, 128, true, 1>), dim3((unsigned)(n / 128)), dim3(256), 0, 0, in, out,
                          n, key, nullptr);
@@ -349,7 +356,9 @@ int main(int argc, char** argv) {
   run("k_load_plain", rw, [&] {
     hipLaunchKernelGGL((kzgpot::k_load<2, 256, false>), dim3(gs), dim3(256), 0, 0, in, out, n, key, nullptr);
   });
-  run("k_load (nt)", rw, [&] { CHECK(kzgpot::launch_load(false, in, out, n, key, nullptr, 0)); });
+  // the product G1 loader: k_load_g1_direct since round 6 (the round-5 product, staged in and out, is
+  // "k_load 1c/l 128" below)
+  run("product G1 (direct)", rw, [&] { CHECK(kzgpot::launch_load(false, in, out, n, key, nullptr, 0)); });
   run("k_load 1c/l 128", rw, [&] {  // one coordinate per lane: 128 points = 256 lanes per block
     hipLaunchKernelGGL((kzgpot::k_load<2, 128, true, 1>), dim3((unsigned)(n / 128)), dim3(256), 0, 0, in, out, n, key,
                        nullptr);
