@@ -22,6 +22,8 @@
 #   gloo8         bench.py --gpus 8 --dist-backend gloo at reduced sizes: the driver's world-8 control
 #                 flow (8 spawned ranks, the rendezvous-store wait, rank 0's e2e at 8 shards, the exit
 #                 code) on the one GPU of the box
+#   overlap       tools/overlap_probe.py (copies on a second stream beside a codec launch, normal and
+#                 highest stream priority: do RCCL-like copy kernels progress during the decode?)
 #   gather1       bench.py --gather-at-1 (the library's RCCL path at one rank)
 #   port          tests/test_gpu_oracle_port.py alone (every point vs the GPU port of the oracle)
 #   campaign      tools/random_campaign.py for 9 minutes (SEED0=... for fresh seeds)
@@ -62,6 +64,7 @@ for step in "$@"; do
              --steps 2 --warmup 1 --bn254-log2 23 --e2e-log2 18 --no-cpu-baseline > ${o}_bench_gloo8.json \
              2> ${o}_bench_gloo8.err; rc=$?; echo "wall_ms $(( ($(date +%s%N) - t0) / 1000000 )) rc $rc" \
              > ${o}_bench_gloo8.wall; (exit $rc) ;;
+    overlap) timeout -k 10 180 python -u tools/overlap_probe.py > ${o}_overlap.json 2> ${o}_overlap.err ;;
     gather1) timeout -k 10 400 python bench.py --gather-at-1 --steps 2 --no-cpu-baseline --no-next-rows \
                > ${o}_bench_gather_at_1.json 2> ${o}_bench_gather_at_1.err ;;
     port) timeout -k 10 1000 python -u -m pytest tests/test_gpu_oracle_port.py -x -v --timeout 900 \
