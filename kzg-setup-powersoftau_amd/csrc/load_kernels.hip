@@ -154,24 +154,28 @@ __global__ void __launch_bounds__(PTS * NC / CPL) k_load(const uint4* __restrict
   }
 }
 
-// G1 with DIRECT input: each lane reads its 48-B coordinate straight from HBM (three 16-B loads
-// at the record stride, through the caches: the three loads of a wave cover its 3 KB of records
-// together) and only the output goes through the LDS slab, so the block has one barrier instead
-// of two. Same bytes as k_load<2, 128, true, 1> (tools/microbench/loader_ceiling.hip verifies
-// them). Measured against the staged kernel on three boxes in round 6: 5.63 / 5.81 / 5.63 TB/s
-// against 5.38 / 5.55 / 5.40 (profiles/r06b, r06d, r06e_loader_ceiling.txt, "DIN plain 128");
-// one round-5 box had it 2 % slower (r05i). With nontemporal loads it is slower everywhere: the
-// three loads of a lane pair's record are the cache lines the streaming hint would evict.
-template <int PTS>
-__global__ void __launch_bounds__(PTS * 2) k_load_g1_direct(const uint4* __restrict__ in, uint4* __restrict__ out,
-                                                            uint64_t n, unsigned long long* __restrict__ first_bad,
-                                                            uint8_t* __restrict__ status) {
-  constexpr int BLK = PTS * 2, RIN = 96, ROUT = 104;  // a point is a lane pair: x, then y with the flags
-  static_assert((PTS * ROUT) % 16 == 0, "slab alignment");
+// DIRECT input, one coordinate per lane (NC lanes per point: G1 x | y, G2 x.c0 | x.c1 | y.c0 |
+// y.c1): each lane reads its 48-B coordinate straight from HBM (three 16-B loads at the record
+// stride, through the caches — the three loads of a wave cover its records together) and only the
+// output goes through the LDS slab, so the block has one barrier instead of two. Same bytes and
+// statuses as k_load (tools/microbench/loader_ceiling.hip verifies the bytes; the loader tests the
+// statuses). G1 (k_load_direct<2, 128>) against the staged kernel on four round-6 boxes: 5.63 /
+// 5.81 / 5.63 / 5.81 TB/s against 5.38 / 5.55 / 5.40 / 5.82 (profiles/r06b, r06d, r06e,
+// r06f_loader_ceiling.txt, "DIN plain 128"); one round-5 box had it 2 % slower (r05i). With
+// nontemporal loads it is slower everywhere: the loads of neighbouring lanes share cache lines.
+// Status order is ark's: the first failing coordinate in x.c0, x.c1, y.c0, (flags), y.c1 order.
+template <int NC, int PTS>
+__global__ void __launch_bounds__(PTS * NC) k_load_direct(const uint4* __restrict__ in, uint4* __restrict__ out,
+                                                          uint64_t n, unsigned long long* __restrict__ first_bad,
+                                                          uint8_t* __restrict__ status) {
+  constexpr int BLK = PTS * NC, RIN = 48 * NC, ROUT = 48 * NC + 8;
+  static_assert(NC == 2 || NC == 4, "G1 or G2");
+  static_assert((PTS * ROUT) % 16 == 0 && BLK % 64 == 0, "slab alignment, whole waves");
   __shared__ uint4 slab[PTS * ROUT / 16];
   const uint64_t base = (uint64_t)blockIdx.x * PTS;
   const int cnt = (int)((n - base) < (uint64_t)PTS ? (n - base) : (uint64_t)PTS);
-  const int t = threadIdx.x, pt = t / 2, h = t % 2;
+  const int t = threadIdx.x, pt = t / NC, h = t % NC;
+  const bool last = h == NC - 1;  // the coordinate that carries the SWFlags
   int st = 0;
   bool finf = false;
   words res;
@@ -179,22 +183,24 @@ __global__ void __launch_bounds__(PTS * 2) k_load_g1_direct(const uint4* __restr
     words c;
     load_le(c, in + (base + pt) * (RIN / 16) + 3 * h);
     const uint32_t yb = c[11] >> 24;
-    finf = h == 1 && (yb & 0x40u);
-    if (h == 1) {
+    finf = last && (yb & 0x40u);
+    if (last) {
       c[11] &= 0x3fffffffu;
-      if ((yb & 0x80u) && finf) st = 6;  // both SWFlags: UnexpectedFlags, before y's range check
+      if ((yb & 0x80u) && finf) st = 6;  // both SWFlags: UnexpectedFlags, before y's last range check
     }
     if (!st && words_geq_p(c)) st = 3;
     words_to_ark_mont(res, c);
   }
-  // the point's status: x's lane first (ark reads x before y's flags), else y's
-  const int other = __shfl_xor(st, 1);
-  st = h == 0 ? (st ? st : other) : (other ? other : st);
+  // the point's status: the first failing coordinate's (lane order = ark's read order)
+  int key = st ? (h << 8) | st : 0xffff;
+#pragma unroll
+  for (int m = 1; m < NC; m <<= 1) key = min(key, __shfl_xor(key, m));
+  st = key == 0xffff ? 0 : key & 0xff;
   if (pt < cnt) {
     uint2* dst = (uint2*)slab + pt * (ROUT / 8) + 6 * h;
 #pragma unroll
     for (int j = 0; j < 6; j++) dst[j] = st ? make_uint2(0, 0) : make_uint2(res[2 * j], res[2 * j + 1]);
-    if (h == 1) {
+    if (last) {
       dst[6] = make_uint2((!st && finf) ? 1u : 0u, 0u);
       report(base + pt, st, first_bad, status);
     }
@@ -222,7 +228,7 @@ hipError_t launch_load(bool g2, const void* d_in, void* d_out, uint64_t n, unsig
                        (uint4*)d_out, n, d_first_bad, d_status);
   } else {
     constexpr int P = 128;  // one coordinate per lane: 256 lanes, 13.3 KB of output slab
-    hipLaunchKernelGGL((k_load_g1_direct<P>), dim3((unsigned)((n + P - 1) / P)), dim3(P * 2), 0, stream,
+    hipLaunchKernelGGL((k_load_direct<2, P>), dim3((unsigned)((n + P - 1) / P)), dim3(P * 2), 0, stream,
                        (const uint4*)d_in, (uint4*)d_out, n, d_first_bad, d_status);
   }
   return hipGetLastError();

@@ -9,7 +9,7 @@
 //   slab_nt       : slab with nontemporal loads and stores
 //   slab_glds_nt  : slab whose input sweep is global_load_lds_dwordx4 (LDS-DMA, no VGPR round trip)
 //                   + nontemporal stores
-//   product G1    : the product kernel (kzgpot::launch_load, G1: k_load_g1_direct since round 6),
+//   product G1    : the product kernel (kzgpot::launch_load, G1: k_load_direct<2, 128> since round 6),
 //                   for the same bytes; "k_load 1c/l 128" is the round-5 product (staged in and out)
 //   k_load_pipe   : an experiment: a resident grid (x f/4 of the occupancy-limited block count)
 //                   walks the slabs grid-stride, prefetching the next slab's input into registers
@@ -123,7 +123,7 @@ __global__ void __launch_bounds__(PTS * NC / CPL) k_load_pipe(const uint4* __res
 // output, and the block's first barrier goes away. G2 (two coordinates per lane): 3.70-3.83 TB/s
 // against 5.56-5.62 for the staged kernel (r05i, r06*). G1 with plain loads: faster than the staged
 // kernel on three of four round-6 boxes (r06b/d/e: 5.63-5.81 against 5.38-5.55 TB/s, equal on
-// r06f), slower on r05i's (5.48 / 5.61) — the product G1 loader since round 6 (k_load_g1_direct in
+// r06f), slower on r05i's (5.48 / 5.61) — the product G1 loader since round 6 (k_load_direct<2, 128> in
 // load_kernels.hip); with nontemporal loads slower everywhere.
 template <int NC, int PTS, bool NT, int CPL>
 __global__ void __launch_bounds__(PTS * NC / CPL) k_load_din(const uint4* __restrict__ in, uint4* __restrict__ out,
@@ -339,6 +339,12 @@ int main(int argc, char** argv) {
       hipLaunchKernelGGL((kzgpot::k_load_din<2, 128, true, 1>), dim3((unsigned)(n / 128)), dim3(256), 0, 0, in, out,
                          n, key, nullptr);
     });
+    cmp("direct 1c/l 32 (G2)", n / 2 * 200, [&] {
+      hipLaunchKernelGGL((kzgpot::k_load<4, 32>), dim3((unsigned)(n / 64)), dim3(64), 0, 0, in, out, n / 2, key, nullptr);
+    }, [&] {
+      hipLaunchKernelGGL((kzgpot::k_load_direct<4, 32>), dim3((unsigned)(n / 64)), dim3(128), 0, 0, in, out, n / 2, key,
+                         nullptr);
+    });
     cmp("DIN 32 (G2)", n / 2 * 200, [&] { CHECK(kzgpot::launch_load(true, in, out, n / 2, key, nullptr, 0)); }, [&] {
       hipLaunchKernelGGL((kzgpot::k_load_din<4, 32, true, 2>), dim3((unsigned)(n / 64)), dim3(64), 0, 0, in, out,
                          n / 2, key, nullptr);
@@ -356,7 +362,7 @@ int main(int argc, char** argv) {
   run("k_load_plain", rw, [&] {
     hipLaunchKernelGGL((kzgpot::k_load<2, 256, false>), dim3(gs), dim3(256), 0, 0, in, out, n, key, nullptr);
   });
-  // the product G1 loader: k_load_g1_direct since round 6 (the round-5 product, staged in and out, is
+  // the product G1 loader: k_load_direct<2, 128> since round 6 (the round-5 product, staged in and out, is
   // "k_load 1c/l 128" below)
   run("product G1 (direct)", rw, [&] { CHECK(kzgpot::launch_load(false, in, out, n, key, nullptr, 0)); });
   run("k_load 1c/l 128", rw, [&] {  // one coordinate per lane: 128 points = 256 lanes per block
@@ -439,6 +445,19 @@ int main(int argc, char** argv) {
   run("k_load<G2> DIN 64", (192.0 + 200.0) * n2, [&] {
     hipLaunchKernelGGL((kzgpot::k_load_din<4, 64, true, 2>), dim3((unsigned)(n2 / 64)), dim3(128), 0, 0, in, out, n2,
                        key, nullptr);
+  });
+  // one coordinate per lane, direct input (k_load_direct<4, PTS>: 4 lanes per point)
+  run("k_load<G2> direct 16", (192.0 + 200.0) * n2, [&] {
+    hipLaunchKernelGGL((kzgpot::k_load_direct<4, 16>), dim3((unsigned)(n2 / 16)), dim3(64), 0, 0, in, out, n2, key,
+                       nullptr);
+  });
+  run("k_load<G2> direct 32", (192.0 + 200.0) * n2, [&] {
+    hipLaunchKernelGGL((kzgpot::k_load_direct<4, 32>), dim3((unsigned)(n2 / 32)), dim3(128), 0, 0, in, out, n2, key,
+                       nullptr);
+  });
+  run("k_load<G2> direct 64", (192.0 + 200.0) * n2, [&] {
+    hipLaunchKernelGGL((kzgpot::k_load_direct<4, 64>), dim3((unsigned)(n2 / 64)), dim3(256), 0, 0, in, out, n2, key,
+                       nullptr);
   });
   run("k_load<G2>plain", (192.0 + 200.0) * n2, [&] {
     hipLaunchKernelGGL((kzgpot::k_load<4, 128, false>), dim3((unsigned)(n2 / 128)), dim3(256), 0, 0, in, out, n2, key,

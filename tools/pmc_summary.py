@@ -33,7 +33,7 @@ KERNELS = {
     "k_g2_codec": "kzgpot::k_g2_codec(",
     "k_g2_decompress": "kzgpot::k_g2_decompress(",
     "k_g2_check": "kzgpot::k_g2_check<(kzgpot::Src)0>",
-    "k_g1_load": "kzgpot::k_load_g1_direct<",  # round 6 (was k_load<2, 128, true, 1>)
+    "k_g1_load": "kzgpot::k_load_direct<2,",  # round 6 (was k_load<2, 128, true, 1>)
     "k_g2_load": "kzgpot::k_load<4, 32",        # one-wave blocks since round 4 (k_load<4, 128> never ran since)
     "k_bn254_g1_decompress": "kzgpot::k_bn254_g1_decompress(",
     "k_g1_transcode": "kzgpot::k_g1_check<(kzgpot::Src)1>",
