@@ -220,12 +220,12 @@ hipError_t launch_load(bool g2, const void* d_in, void* d_out, uint64_t n, unsig
                        uint8_t* d_status, hipStream_t stream) {
   if (n == 0) return hipSuccess;
   if (g2) {
-    // one wave per block (32 points, 6.4 KB of slab): no block barrier makes a wave wait for three
-    // others, 5.26 -> 5.59 TB/s against 128-point blocks (profiles/r04j_loader_ceiling.txt; for G1
-    // the block size is neutral: 5.50-5.53 TB/s at 32 / 64 / 128 points)
-    constexpr int P = 32;
-    hipLaunchKernelGGL((k_load<4, P>), dim3((unsigned)((n + P - 1) / P)), dim3(P * 2), 0, stream, (const uint4*)d_in,
-                       (uint4*)d_out, n, d_first_bad, d_status);
+    // one coordinate per lane, direct input: 5.66-5.67 TB/s at 16 / 32 / 64-point blocks against
+    // 5.55-5.59 for the staged lane-pair kernel in one-wave blocks (k_load<4, 32>, the product from
+    // round 4 to 6: profiles/r06h_loader_ceiling.txt, same bytes)
+    constexpr int P = 32;  // 128 lanes, 6.4 KB of output slab
+    hipLaunchKernelGGL((k_load_direct<4, P>), dim3((unsigned)((n + P - 1) / P)), dim3(P * 4), 0, stream,
+                       (const uint4*)d_in, (uint4*)d_out, n, d_first_bad, d_status);
   } else {
     constexpr int P = 128;  // one coordinate per lane: 256 lanes, 13.3 KB of output slab
     hipLaunchKernelGGL((k_load_direct<2, P>), dim3((unsigned)((n + P - 1) / P)), dim3(P * 2), 0, stream,

@@ -9,8 +9,9 @@
 //   slab_nt       : slab with nontemporal loads and stores
 //   slab_glds_nt  : slab whose input sweep is global_load_lds_dwordx4 (LDS-DMA, no VGPR round trip)
 //                   + nontemporal stores
-//   product G1    : the product kernel (kzgpot::launch_load, G1: k_load_direct<2, 128> since round 6),
-//                   for the same bytes; "k_load 1c/l 128" is the round-5 product (staged in and out)
+//   product G1/G2 : the product kernels (kzgpot::launch_load: k_load_direct<2, 128> / <4, 32> since
+//                   round 6), for the same bytes; "k_load 1c/l 128" / "k_load<G2> 32" are the round-5
+//                   products (staged in and out)
 //   k_load_pipe   : an experiment: a resident grid (x f/4 of the occupancy-limited block count)
 //                   walks the slabs grid-stride, prefetching the next slab's input into registers
 //                   while it converts and stores the current one. Slower than letting the hardware
@@ -339,11 +340,8 @@ int main(int argc, char** argv) {
       hipLaunchKernelGGL((kzgpot::k_load_din<2, 128, true, 1>), dim3((unsigned)(n / 128)), dim3(256), 0, 0, in, out,
                          n, key, nullptr);
     });
-    cmp("direct 1c/l 32 (G2)", n / 2 * 200, [&] {
+    cmp("staged 32 (G2)", n / 2 * 200, [&] { CHECK(kzgpot::launch_load(true, in, out, n / 2, key, nullptr, 0)); }, [&] {
       hipLaunchKernelGGL((kzgpot::k_load<4, 32>), dim3((unsigned)(n / 64)), dim3(64), 0, 0, in, out, n / 2, key, nullptr);
-    }, [&] {
-      hipLaunchKernelGGL((kzgpot::k_load_direct<4, 32>), dim3((unsigned)(n / 64)), dim3(128), 0, 0, in, out, n / 2, key,
-                         nullptr);
     });
     cmp("DIN 32 (G2)", n / 2 * 200, [&] { CHECK(kzgpot::launch_load(true, in, out, n / 2, key, nullptr, 0)); }, [&] {
       hipLaunchKernelGGL((kzgpot::k_load_din<4, 32, true, 2>), dim3((unsigned)(n / 64)), dim3(64), 0, 0, in, out,
@@ -429,7 +427,7 @@ int main(int argc, char** argv) {
       hipLaunchKernelGGL((kzgpot::k_load_pipe<4, 128, 2>), dim3(g), dim3(256), 0, 0, in, out, n2, key, nullptr);
     });
   }
-  run("k_load<G2>", (192.0 + 200.0) * n2 * 1.0, [&] { CHECK(kzgpot::launch_load(true, in, out, n2, key, nullptr, 0)); });
+  run("product G2 (direct)", (192.0 + 200.0) * n2, [&] { CHECK(kzgpot::launch_load(true, in, out, n2, key, nullptr, 0)); });
   run("k_load<G2> 32", (192.0 + 200.0) * n2, [&] {
     hipLaunchKernelGGL((kzgpot::k_load<4, 32, true, 2>), dim3((unsigned)(n2 / 32)), dim3(64), 0, 0, in, out, n2, key,
                        nullptr);

@@ -34,12 +34,12 @@ KERNELS = {
     "k_g2_decompress": "kzgpot::k_g2_decompress(",
     "k_g2_check": "kzgpot::k_g2_check<(kzgpot::Src)0>",
     "k_g1_load": "kzgpot::k_load_direct<2,",  # round 6 (was k_load<2, 128, true, 1>)
-    "k_g2_load": "kzgpot::k_load<4, 32",        # one-wave blocks since round 4 (k_load<4, 128> never ran since)
+    "k_g2_load": "kzgpot::k_load_direct<4,",  # round 6 (was k_load<4, 32> from round 4, k_load<4, 128> before)
     "k_bn254_g1_decompress": "kzgpot::k_bn254_g1_decompress(",
     "k_g1_transcode": "kzgpot::k_g1_check<(kzgpot::Src)1>",
     "k_g2_transcode": "kzgpot::k_g2_check<(kzgpot::Src)1>",
 }
-LANES_PER_POINT = {"k_g1_load": 2, "k_g2_load": 2}  # the loaders run a point as a lane pair (load_kernels.hip)
+LANES_PER_POINT = {"k_g1_load": 2, "k_g2_load": 4}  # the loaders run one coordinate per lane (load_kernels.hip)
 SIMDS_PER_XCD = 32 * 4  # GRBM_GUI_ACTIVE is summed over the 8 XCDs (one clock each); 32 CUs x 4 SIMDs per XCD
 
 
