@@ -12,8 +12,9 @@
 // padding to 8 B: G1 104 B (x 48 | y 48 | inf 1 | pad 7), G2 200 B (x.c0 | x.c1 | y.c0 | y.c1 |
 // inf | pad). Rejected points are zero-filled.
 //
-// HBM-bound: 96 B in + 104 B out per G1 point against 2 Fp multiplies; global traffic is staged
-// through LDS so that it is fully coalesced.
+// HBM-bound: 96 B in + 104 B out per G1 point against 2 Fp multiplies. The product kernel is
+// k_load_direct (below): each lane reads one coordinate straight from HBM, and the output is staged
+// through LDS so that its stores are fully coalesced.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -62,6 +63,7 @@ KZG_DEV void words_to_ark_mont(words& out, const words& w) {
   fp_to_words(out, x);
 }
 
+// k_load: the product loader of rounds 2-5, kept for tools/microbench/loader_ceiling.hip.
 // One block handles PTS consecutive points. Records are packed at 96 / 192 B (in) and 104 / 200
 // B (out), which lane-per-record accesses would touch at a 96-200 B stride; instead the block
 // stages its whole input and output slab through LDS so that every global access is a
@@ -163,6 +165,8 @@ __global__ void __launch_bounds__(PTS * NC / CPL) k_load(const uint4* __restrict
 // 5.81 / 5.63 / 5.81 TB/s against 5.38 / 5.55 / 5.40 / 5.82 (profiles/r06b, r06d, r06e,
 // r06f_loader_ceiling.txt, "DIN plain 128"); one round-5 box had it 2 % slower (r05i). With
 // nontemporal loads it is slower everywhere: the loads of neighbouring lanes share cache lines.
+// G2 (k_load_direct<4, 32>) against the staged k_load<4, 32>: 5.65-5.66 against 5.56-5.57 TB/s
+// (profiles/r06h, r06i_loader_ceiling.txt).
 // Status order is ark's: the first failing coordinate in x.c0, x.c1, y.c0, (flags), y.c1 order.
 template <int NC, int PTS>
 __global__ void __launch_bounds__(PTS * NC) k_load_direct(const uint4* __restrict__ in, uint4* __restrict__ out,
