@@ -235,3 +235,36 @@ def test_fuzz_loader(gpu, g2):
     assert list(r.status) == want_st
     assert r.out == b"".join(want_out)
     assert want_st.count(0) > 1000 if not g2 else want_st.count(0) > 500
+
+
+@pytest.mark.parametrize("g2", [False, True], ids=["g1", "g2"])
+def test_loader_fault_precedence_and_tails(gpu, g2):
+    """Records with several faults at once (coordinates >= p in any subset, with and without flag
+    damage on y's top byte), so the per-record status must be the FIRST fault in ark's read order
+    (x[.c0, .c1], then y[.c0], the flags, y[.c1]) — the direct loader merges its lanes' statuses by
+    lane order — at stream lengths around the kernels' 128- / 32-point blocks (ragged tails, single
+    records) and the first_bad of each stream, against the Python oracle."""
+    O = pytest.importorskip("kzgpot_oracle")
+    rng = random.Random(900 + g2)
+    nc = 4 if g2 else 2
+    fn = O.g2_deserialize_unchecked_point if g2 else O.g1_deserialize_unchecked_point
+    rout = 200 if g2 else 104
+    recs = []
+    for mask in range(1 << nc):
+        for flags in (0x00, 0x40, 0x80, 0xC0):
+            coords = [P + rng.randrange(1 << 40) if mask >> c & 1 else _rand_fp(rng) for c in range(nc)]
+            b = bytearray(b"".join(c.to_bytes(48, "little") for c in coords))
+            b[-1] |= flags
+            recs.append(bytes(b))
+    ok = [rec for rec in recs if fn(rec)[0] == 0]
+    assert ok and len({fn(rec)[0] for rec in recs}) >= 3  # accepted, InvalidData and UnexpectedFlags all occur
+    block = 32 if g2 else 128
+    for n in (1, 2, block - 1, block, block + 1, 2 * block + 3, len(recs)):
+        stream = [recs[(7 * i + n) % len(recs)] if i % 3 == 0 else ok[i % len(ok)] for i in range(n)]
+        r = gpu.deserialize_unchecked(b"".join(stream), g2=g2, want_status=True)
+        want = [fn(rec) for rec in stream]
+        want_st = [st for st, _ in want]
+        assert list(r.status) == want_st, n
+        assert r.out == b"".join(out if st == 0 else bytes(rout) for st, out in want), n
+        bad = [i for i, s in enumerate(want_st) if s]
+        assert r.first_bad == (bad[0] if bad else -1), n
