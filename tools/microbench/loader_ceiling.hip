@@ -180,6 +180,67 @@ __global__ void __launch_bounds__(PTS * NC / CPL) k_load_din(const uint4* __rest
   uint4* dst = (uint4*)((uint8_t*)out + base * ROUT);  // full blocks only (n is a multiple of PTS here)
   for (int k = t; k < PTS * ROUT / 16; k += BLK) st_stream(dst + k, slab[k]);
 }
+
+// k_load_direct with DIRECT OUTPUT too (round 6 experiment): no LDS slab and no barrier — each lane
+// writes its converted 48-B coordinate straight to its place in the output record (8-B aligned at
+// the 104- / 200-B record stride), the flags lane also the 8-B infinity word, and the L2 merges
+// neighbouring lanes' pieces into whole lines before write-back. ST 0: plain 8-B stores; 1:
+// nontemporal 8-B stores; 2: 16-B stores at 4-B alignment (unaligned-access mode). The compiler
+// emits three 16-B stores per lane in every case. Measured (profiles/r06m_loader_ceiling.txt, bytes
+// equal): G1 4.69 TB/s, G2 4.40 (4.90 at 64-point blocks) against 5.66 / 5.52 for the product on
+// the same box; with nontemporal stores 1.9-2.3 TB/s. Staging the output pays: NOT in the product.
+struct __attribute__((packed, aligned(4))) u4a {
+  uint32_t x, y, z, w;
+};
+template <int NC, int PTS, int ST>
+__global__ void __launch_bounds__(PTS * NC) k_load_dd(const uint4* __restrict__ in, uint4* __restrict__ out, uint64_t n,
+                                                      unsigned long long* __restrict__ first_bad, uint8_t* status) {
+  constexpr int RIN = 48 * NC, ROUT = 48 * NC + 8;
+  const uint64_t base = (uint64_t)blockIdx.x * PTS;
+  const int t = threadIdx.x, pt = t / NC, h = t % NC;
+  const bool last = h == NC - 1, live = base + pt < n;
+  int st = 0;
+  bool finf = false;
+  words res;
+  if (live) {
+    words c;
+    load_le(c, in + (base + pt) * (RIN / 16) + 3 * h);
+    const uint32_t yb = c[11] >> 24;
+    finf = last && (yb & 0x40u);
+    if (last) {
+      c[11] &= 0x3fffffffu;
+      if ((yb & 0x80u) && finf) st = 6;
+    }
+    if (!st && words_geq_p(c)) st = 3;
+    words_to_ark_mont(res, c);
+  }
+  int key = st ? (h << 8) | st : 0xffff;
+#pragma unroll
+  for (int m = 1; m < NC; m <<= 1) key = min(key, __shfl_xor(key, m));
+  st = key == 0xffff ? 0 : key & 0xff;
+  if (!live) return;
+  uint8_t* rec = (uint8_t*)out + (base + pt) * ROUT + 48 * h;
+  if (st)
+#pragma unroll
+    for (int k = 0; k < 12; k++) res[k] = 0;
+  if (ST == 2) {
+    u4a* d = (u4a*)rec;
+#pragma unroll
+    for (int j = 0; j < 3; j++) d[j] = u4a{res[4 * j], res[4 * j + 1], res[4 * j + 2], res[4 * j + 3]};
+  } else {
+    uint2* d = (uint2*)rec;
+#pragma unroll
+    for (int j = 0; j < 6; j++) {
+      const uint2 v = make_uint2(res[2 * j], res[2 * j + 1]);
+      if (ST == 1) __builtin_nontemporal_store(*(const uint64_t*)&v, (uint64_t*)(d + j));
+      else d[j] = v;
+    }
+  }
+  if (last) {
+    *(uint2*)(rec + 48) = make_uint2((!st && finf) ? 1u : 0u, 0u);
+    report(base + pt, st, first_bad, status);
+  }
+}
 }  // namespace kzgpot
 
 #define CHECK(x)                                                                                 \
@@ -347,6 +408,22 @@ int main(int argc, char** argv) {
       hipLaunchKernelGGL((kzgpot::k_load_din<4, 32, true, 2>), dim3((unsigned)(n / 64)), dim3(64), 0, 0, in, out,
                          n / 2, key, nullptr);
     });
+    cmp("DD 128 (G1)", n * 104, [&] { CHECK(kzgpot::launch_load(false, in, out, n, key, nullptr, 0)); }, [&] {
+      hipLaunchKernelGGL((kzgpot::k_load_dd<2, 128, 0>), dim3((unsigned)(n / 128)), dim3(256), 0, 0, in, out, n, key,
+                         nullptr);
+    });
+    cmp("DD16 128 (G1)", n * 104, [&] { CHECK(kzgpot::launch_load(false, in, out, n, key, nullptr, 0)); }, [&] {
+      hipLaunchKernelGGL((kzgpot::k_load_dd<2, 128, 2>), dim3((unsigned)(n / 128)), dim3(256), 0, 0, in, out, n, key,
+                         nullptr);
+    });
+    cmp("DD 32 (G2)", n / 2 * 200, [&] { CHECK(kzgpot::launch_load(true, in, out, n / 2, key, nullptr, 0)); }, [&] {
+      hipLaunchKernelGGL((kzgpot::k_load_dd<4, 32, 0>), dim3((unsigned)(n / 64)), dim3(128), 0, 0, in, out, n / 2, key,
+                         nullptr);
+    });
+    cmp("DD16 32 (G2)", n / 2 * 200, [&] { CHECK(kzgpot::launch_load(true, in, out, n / 2, key, nullptr, 0)); }, [&] {
+      hipLaunchKernelGGL((kzgpot::k_load_dd<4, 32, 2>), dim3((unsigned)(n / 64)), dim3(128), 0, 0, in, out, n / 2, key,
+                         nullptr);
+    });
     free(want);
     free(got);
   }
@@ -363,6 +440,19 @@ int main(int argc, char** argv) {
   // the product G1 loader: k_load_direct<2, 128> since round 6 (the round-5 product, staged in and out, is
   // "k_load 1c/l 128" below)
   run("product G1 (direct)", rw, [&] { CHECK(kzgpot::launch_load(false, in, out, n, key, nullptr, 0)); });
+  // direct output (no slab): plain / nontemporal 8-B stores, 16-B stores at 4-B alignment
+  run("DD G1 128 st8", rw, [&] {
+    hipLaunchKernelGGL((kzgpot::k_load_dd<2, 128, 0>), dim3((unsigned)(n / 128)), dim3(256), 0, 0, in, out, n, key, nullptr);
+  });
+  run("DD G1 128 nt8", rw, [&] {
+    hipLaunchKernelGGL((kzgpot::k_load_dd<2, 128, 1>), dim3((unsigned)(n / 128)), dim3(256), 0, 0, in, out, n, key, nullptr);
+  });
+  run("DD G1 128 st16", rw, [&] {
+    hipLaunchKernelGGL((kzgpot::k_load_dd<2, 128, 2>), dim3((unsigned)(n / 128)), dim3(256), 0, 0, in, out, n, key, nullptr);
+  });
+  run("DD G1 32 st8", rw, [&] {
+    hipLaunchKernelGGL((kzgpot::k_load_dd<2, 32, 0>), dim3((unsigned)(n / 32)), dim3(64), 0, 0, in, out, n, key, nullptr);
+  });
   run("k_load 1c/l 128", rw, [&] {  // one coordinate per lane: 128 points = 256 lanes per block
     hipLaunchKernelGGL((kzgpot::k_load<2, 128, true, 1>), dim3((unsigned)(n / 128)), dim3(256), 0, 0, in, out, n, key,
                        nullptr);
@@ -428,6 +518,18 @@ int main(int argc, char** argv) {
     });
   }
   run("product G2 (direct)", (192.0 + 200.0) * n2, [&] { CHECK(kzgpot::launch_load(true, in, out, n2, key, nullptr, 0)); });
+  run("DD G2 32 st8", (192.0 + 200.0) * n2, [&] {
+    hipLaunchKernelGGL((kzgpot::k_load_dd<4, 32, 0>), dim3((unsigned)(n2 / 32)), dim3(128), 0, 0, in, out, n2, key, nullptr);
+  });
+  run("DD G2 32 nt8", (192.0 + 200.0) * n2, [&] {
+    hipLaunchKernelGGL((kzgpot::k_load_dd<4, 32, 1>), dim3((unsigned)(n2 / 32)), dim3(128), 0, 0, in, out, n2, key, nullptr);
+  });
+  run("DD G2 32 st16", (192.0 + 200.0) * n2, [&] {
+    hipLaunchKernelGGL((kzgpot::k_load_dd<4, 32, 2>), dim3((unsigned)(n2 / 32)), dim3(128), 0, 0, in, out, n2, key, nullptr);
+  });
+  run("DD G2 64 st8", (192.0 + 200.0) * n2, [&] {
+    hipLaunchKernelGGL((kzgpot::k_load_dd<4, 64, 0>), dim3((unsigned)(n2 / 64)), dim3(256), 0, 0, in, out, n2, key, nullptr);
+  });
   run("k_load<G2> 32", (192.0 + 200.0) * n2, [&] {
     hipLaunchKernelGGL((kzgpot::k_load<4, 32, true, 2>), dim3((unsigned)(n2 / 32)), dim3(64), 0, 0, in, out, n2, key,
                        nullptr);
