@@ -17,7 +17,13 @@ import re
 import sys
 
 WANT = {"k_copy16": "copy16 (plain 16-B copy, 192 B/pt)", "k_slab<true, true, false>": "slab_nt (the staged pattern, no arithmetic)",
-        "k_load<2, 128, true, 1>": "k_load<G1> (product)", "k_load<4, 128, true, 2>": "k_load<G2> (product)"}
+        "k_load_direct<2, 128>": "k_load_direct<2, 128> (product G1 since round 6)",
+        "k_load_direct<4, 32>": "k_load_direct<4, 32> (product G2 since round 6)",
+        "k_load<2, 128, true, 1>": "k_load<G1> (staged, product to round 5)",
+        "k_load<4, 32, true, 2>": "k_load<G2> 32 (staged, product rounds 4-6)",
+        "k_load<4, 128, true, 2>": "k_load<G2> 128 (staged, product to round 3)",
+        "k_load_dd<2, 128, 0>": "k_load_dd<2, 128> (direct output, experiment)",
+        "k_load_dd<4, 32, 0>": "k_load_dd<4, 32> (direct output, experiment)"}
 
 
 def main():
@@ -27,7 +33,7 @@ def main():
         for r in csv.DictReader(open(f)):
             name = re.sub(r"^(void )?(kzgpot::)?", "", r["Kernel_Name"]).split("(")[0]
             for pat, label in WANT.items():
-                if name == pat or name.startswith(pat):
+                if name == pat:
                     tot[label][r["Counter_Name"]] += float(r["Counter_Value"])
     out = {"source": f"tools/pmc_loader_stalls.sh -> {root}", "kernels": {}}
     for label, c in tot.items():

@@ -1,6 +1,6 @@
 #!/usr/bin/env bash
 # Per-wave stall attribution of the loader against its staged pattern: the
-# loader_ceiling microbenchmark's copy16 / slab_nt / k_load / k_load<G2> kernels under two SQ PMC
+# loader_ceiling microbenchmark's copy16 / slab_nt / product (k_load_direct) / staged k_load kernels under two SQ PMC
 # passes (run through gpurun from the repo root; build tools/microbench/bin/loader_ceiling first).
 set -uo pipefail
 out=$GRAFT_REPO_ROOT/gpurun_out/loader_stalls
