@@ -32,6 +32,12 @@ namespace kzgpot {
 //   (mod p), and S < 12 x 2^32 p makes it < 1.000001 p, so one conditional subtraction finishes.
 // 196 product mads and no word <-> limb conversion of the input, against fp_from_words + a
 // 392-mad fp_mul by 2^384 R. Any 384-bit input keeps every bound (the caller rejects x >= p).
+// The final conditional subtraction is needed only when the result's top limb reaches p's
+// (the value is < 1.000001 p, so a top limb below p's means a value below p; a uniform value hits
+// it with probability ~1e-5): FILTER runs it in a wave-uniform branch taken only when some lane of
+// the wave needs it, 56 instructions per lane saved otherwise. FILTER = false: the r06n form (the
+// microbenchmark's A sides).
+template <bool FILTER = true>
 KZG_DEV void words_to_ark_mont(words& out, const words& w) {
   constexpr int N = BlsFp::NL;
   uint64_t col[N + 1];
@@ -59,9 +65,10 @@ KZG_DEV void words_to_ark_mont(words& out, const words& w) {
     c >>= BlsFp::LB;
   }
   x.v[N - 1] = (uint32_t)c;
-  fp_reduce_once(x, x);
+  if (!FILTER || __ballot(x.v[N - 1] >= BlsFp::P[N - 1])) fp_reduce_once(x, x);
   fp_to_words(out, x);
 }
+
 
 // k_load: the product loader of rounds 2-5, kept for tools/microbench/loader_ceiling.hip.
 // One block handles PTS consecutive points. Records are packed at 96 / 192 B (in) and 104 / 200
@@ -166,9 +173,14 @@ __global__ void __launch_bounds__(PTS * NC / CPL) k_load(const uint4* __restrict
 // r06f_loader_ceiling.txt, "DIN plain 128"); one round-5 box had it 2 % slower (r05i). With
 // nontemporal loads it is slower everywhere: the loads of neighbouring lanes share cache lines.
 // G2 (k_load_direct<4, 32>) against the staged k_load<4, 32>: 5.65-5.66 against 5.56-5.57 TB/s
-// (profiles/r06h, r06i_loader_ceiling.txt).
+// (profiles/r06h, r06i_loader_ceiling.txt). The loaders keep the SIMDs issuing VALU ~83 % of their
+// cycles (profiles/r06n_loader_stalls.json), so VALU instructions cost bandwidth here: every lane
+// converting (no zero-initialised results for a tail block's idle lanes), a branch for the rare
+// zero-fill and the filtered conditional subtraction (words_to_ark_mont<true>) took G1 5.70-5.72 ->
+// 5.81-5.87 and G2 5.57-5.59 -> 5.72-5.88 TB/s on one box (r06s_loader_ceiling.txt, bytes equal; the
+// filter alone +0.1-3 %). A wave-uniform filter on the input range test measured slower (r06q).
 // Status order is ark's: the first failing coordinate in x.c0, x.c1, y.c0, (flags), y.c1 order.
-template <int NC, int PTS>
+template <int NC, int PTS, bool FILTER = true>  // FILTER: words_to_ark_mont's (false: r06s's A side)
 __global__ void __launch_bounds__(PTS * NC) k_load_direct(const uint4* __restrict__ in, uint4* __restrict__ out,
                                                           uint64_t n, unsigned long long* __restrict__ first_bad,
                                                           uint8_t* __restrict__ status) {
@@ -180,30 +192,32 @@ __global__ void __launch_bounds__(PTS * NC) k_load_direct(const uint4* __restric
   const int cnt = (int)((n - base) < (uint64_t)PTS ? (n - base) : (uint64_t)PTS);
   const int t = threadIdx.x, pt = t / NC, h = t % NC;
   const bool last = h == NC - 1;  // the coordinate that carries the SWFlags
+  // Every lane converts: the idle lanes of a ragged tail block re-read the block's last record and
+  // write nothing, so no lane needs zero-initialised results (13 fewer VALU per lane).
+  const bool live = pt < cnt;
+  words c, res;
+  load_le(c, in + (base + (live ? pt : cnt - 1)) * (RIN / 16) + 3 * h);
+  const uint32_t yb = c[11] >> 24;
+  const bool finf = last && (yb & 0x40u);
   int st = 0;
-  bool finf = false;
-  words res;
-  if (pt < cnt) {
-    words c;
-    load_le(c, in + (base + pt) * (RIN / 16) + 3 * h);
-    const uint32_t yb = c[11] >> 24;
-    finf = last && (yb & 0x40u);
-    if (last) {
-      c[11] &= 0x3fffffffu;
-      if ((yb & 0x80u) && finf) st = 6;  // both SWFlags: UnexpectedFlags, before y's last range check
-    }
-    if (!st && words_geq_p(c)) st = 3;
-    words_to_ark_mont(res, c);
+  if (last) {
+    c[11] &= 0x3fffffffu;
+    if ((yb & 0x80u) && finf) st = 6;  // both SWFlags: UnexpectedFlags, before y's last range check
   }
+  if (!st && words_geq_p(c)) st = 3;
+  words_to_ark_mont<FILTER>(res, c);
   // the point's status: the first failing coordinate's (lane order = ark's read order)
   int key = st ? (h << 8) | st : 0xffff;
 #pragma unroll
   for (int m = 1; m < NC; m <<= 1) key = min(key, __shfl_xor(key, m));
   st = key == 0xffff ? 0 : key & 0xff;
-  if (pt < cnt) {
+  if (live) {
     uint2* dst = (uint2*)slab + pt * (ROUT / 8) + 6 * h;
 #pragma unroll
-    for (int j = 0; j < 6; j++) dst[j] = st ? make_uint2(0, 0) : make_uint2(res[2 * j], res[2 * j + 1]);
+    for (int j = 0; j < 6; j++) dst[j] = make_uint2(res[2 * j], res[2 * j + 1]);
+    if (st)  // rare: a rejected point is zero-filled (a branch instead of 12 selects per lane)
+#pragma unroll
+      for (int j = 0; j < 6; j++) dst[j] = make_uint2(0, 0);
     if (last) {
       dst[6] = make_uint2((!st && finf) ? 1u : 0u, 0u);
       report(base + pt, st, first_bad, status);

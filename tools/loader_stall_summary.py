@@ -17,8 +17,10 @@ import re
 import sys
 
 WANT = {"k_copy16": "copy16 (plain 16-B copy, 192 B/pt)", "k_slab<true, true, false>": "slab_nt (the staged pattern, no arithmetic)",
-        "k_load_direct<2, 128>": "k_load_direct<2, 128> (product G1 since round 6)",
-        "k_load_direct<4, 32>": "k_load_direct<4, 32> (product G2 since round 6)",
+        "k_load_direct<2, 128, true>": "k_load_direct<2, 128> (product G1 since round 6)",
+        "k_load_direct<4, 32, true>": "k_load_direct<4, 32> (product G2 since round 6)",
+        "k_load_direct<2, 128>": "k_load_direct<2, 128> (r06h-r06n form)",
+        "k_load_direct<4, 32>": "k_load_direct<4, 32> (r06h-r06n form)",
         "k_load<2, 128, true, 1>": "k_load<G1> (staged, product to round 5)",
         "k_load<4, 32, true, 2>": "k_load<G2> 32 (staged, product rounds 4-6)",
         "k_load<4, 128, true, 2>": "k_load<G2> 128 (staged, product to round 3)",

@@ -241,6 +241,59 @@ __global__ void __launch_bounds__(PTS * NC) k_load_dd(const uint4* __restrict__ 
     report(base + pt, st, first_bad, status);
   }
 }
+
+// k_load_direct as it ran in r06h-r06n (the A side of the r06o/r06q changes): tail-block lanes
+// skipped the conversion (so the compiler zero-initialised their results), a rejected point was
+// zero-filled by 12 selects per lane instead of a branch, and the range test and the conversion's
+// conditional subtraction ran in every lane (no wave-uniform filter).
+template <int NC, int PTS>
+__global__ void __launch_bounds__(PTS * NC) k_load_direct_r06n(const uint4* __restrict__ in, uint4* __restrict__ out,
+                                                               uint64_t n, unsigned long long* __restrict__ first_bad,
+                                                               uint8_t* __restrict__ status) {
+  constexpr int BLK = PTS * NC, RIN = 48 * NC, ROUT = 48 * NC + 8;
+  __shared__ uint4 slab[PTS * ROUT / 16];
+  const uint64_t base = (uint64_t)blockIdx.x * PTS;
+  const int cnt = (int)((n - base) < (uint64_t)PTS ? (n - base) : (uint64_t)PTS);
+  const int t = threadIdx.x, pt = t / NC, h = t % NC;
+  const bool last = h == NC - 1;
+  int st = 0;
+  bool finf = false;
+  words res;
+  if (pt < cnt) {
+    words c;
+    load_le(c, in + (base + pt) * (RIN / 16) + 3 * h);
+    const uint32_t yb = c[11] >> 24;
+    finf = last && (yb & 0x40u);
+    if (last) {
+      c[11] &= 0x3fffffffu;
+      if ((yb & 0x80u) && finf) st = 6;
+    }
+    if (!st && words_geq_p(c)) st = 3;
+    words_to_ark_mont<false>(res, c);
+  }
+  int key = st ? (h << 8) | st : 0xffff;
+#pragma unroll
+  for (int m = 1; m < NC; m <<= 1) key = min(key, __shfl_xor(key, m));
+  st = key == 0xffff ? 0 : key & 0xff;
+  if (pt < cnt) {
+    uint2* dst = (uint2*)slab + pt * (ROUT / 8) + 6 * h;
+#pragma unroll
+    for (int j = 0; j < 6; j++) dst[j] = st ? make_uint2(0, 0) : make_uint2(res[2 * j], res[2 * j + 1]);
+    if (last) {
+      dst[6] = make_uint2((!st && finf) ? 1u : 0u, 0u);
+      report(base + pt, st, first_bad, status);
+    }
+  }
+  __syncthreads();
+  if (cnt == PTS) {
+    uint4* dst = (uint4*)((uint8_t*)out + base * ROUT);
+    for (int k = t; k < PTS * ROUT / 16; k += BLK) st_stream(dst + k, slab[k]);
+  } else {
+    uint2* dst = (uint2*)out + base * (ROUT / 8);
+    const uint2* s2 = (const uint2*)slab;
+    for (int k = t; k < cnt * (ROUT / 8); k += BLK) dst[k] = s2[k];
+  }
+}
 }  // namespace kzgpot
 
 #define CHECK(x)                                                                                 \
@@ -424,6 +477,10 @@ int main(int argc, char** argv) {
       hipLaunchKernelGGL((kzgpot::k_load_dd<4, 32, 2>), dim3((unsigned)(n / 64)), dim3(128), 0, 0, in, out, n / 2, key,
                          nullptr);
     });
+    cmp("r06n direct (G1)", n * 104, [&] { CHECK(kzgpot::launch_load(false, in, out, n, key, nullptr, 0)); }, [&] {
+      hipLaunchKernelGGL((kzgpot::k_load_direct_r06n<2, 128>), dim3((unsigned)(n / 128)), dim3(256), 0, 0, in, out, n,
+                         key, nullptr);
+    });
     free(want);
     free(got);
   }
@@ -440,6 +497,15 @@ int main(int argc, char** argv) {
   // the product G1 loader: k_load_direct<2, 128> since round 6 (the round-5 product, staged in and out, is
   // "k_load 1c/l 128" below)
   run("product G1 (direct)", rw, [&] { CHECK(kzgpot::launch_load(false, in, out, n, key, nullptr, 0)); });
+  run("direct G1 r06n", rw, [&] {
+    hipLaunchKernelGGL((kzgpot::k_load_direct_r06n<2, 128>), dim3((unsigned)(n / 128)), dim3(256), 0, 0, in, out, n, key,
+                       nullptr);
+  });
+  run("direct G1 nofilter", rw, [&] {
+    hipLaunchKernelGGL((kzgpot::k_load_direct<2, 128, false>), dim3((unsigned)(n / 128)), dim3(256), 0, 0, in, out, n,
+                       key, nullptr);
+  });
+  run("product G1 (again)", rw, [&] { CHECK(kzgpot::launch_load(false, in, out, n, key, nullptr, 0)); });
   // direct output (no slab): plain / nontemporal 8-B stores, 16-B stores at 4-B alignment
   run("DD G1 128 st8", rw, [&] {
     hipLaunchKernelGGL((kzgpot::k_load_dd<2, 128, 0>), dim3((unsigned)(n / 128)), dim3(256), 0, 0, in, out, n, key, nullptr);
@@ -518,6 +584,15 @@ int main(int argc, char** argv) {
     });
   }
   run("product G2 (direct)", (192.0 + 200.0) * n2, [&] { CHECK(kzgpot::launch_load(true, in, out, n2, key, nullptr, 0)); });
+  run("direct G2 r06n", (192.0 + 200.0) * n2, [&] {
+    hipLaunchKernelGGL((kzgpot::k_load_direct_r06n<4, 32>), dim3((unsigned)(n2 / 32)), dim3(128), 0, 0, in, out, n2, key,
+                       nullptr);
+  });
+  run("direct G2 nofilter", (192.0 + 200.0) * n2, [&] {
+    hipLaunchKernelGGL((kzgpot::k_load_direct<4, 32, false>), dim3((unsigned)(n2 / 32)), dim3(128), 0, 0, in, out, n2,
+                       key, nullptr);
+  });
+  run("product G2 (again)", (192.0 + 200.0) * n2, [&] { CHECK(kzgpot::launch_load(true, in, out, n2, key, nullptr, 0)); });
   run("DD G2 32 st8", (192.0 + 200.0) * n2, [&] {
     hipLaunchKernelGGL((kzgpot::k_load_dd<4, 32, 0>), dim3((unsigned)(n2 / 32)), dim3(128), 0, 0, in, out, n2, key, nullptr);
   });
