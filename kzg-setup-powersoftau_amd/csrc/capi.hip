@@ -222,6 +222,56 @@ int decode_key(uint64_t key, int64_t* first_bad) {
   return -(int)(key & 0xff);
 }
 
+// The chunks of a host-buffer call (run_host). Only the first chunk's input copy and the last
+// chunk's output copy are exposed (every other copy runs while a kernel does), so a long call
+// starts with a 2^17-point chunk (one wave of blocks on 256 CUs) growing x4 per chunk below cmax,
+// and ends with chunks halving from <= cmax / 2 down to 2^17: chunk k's output copy then hides
+// behind chunk k + 1's kernel, which is at least half as long, and the exposed copies are of
+// 2^17-point chunks instead of cmax-point ones (2^25 G1 points: 100 + 201 MB at cmax = 2^21). A
+// call too short for both ramps keeps equal chunks. Chunks are multiples of 256 points but one.
+struct ChunkPlan {
+  size_t n = 0, cmax = 0, first = 0;  // equal-chunk plan: [first, cmax, cmax, ..., tail]
+  bool ramp = false;
+  size_t up = 0, mid = 0, down = 0, sum_up = 0, rest = 0;  // ramp plan: up x4, mid x cmax, down /2
+  static constexpr size_t kMin = (size_t)1 << 17;
+  ChunkPlan(size_t n_, bool small_first) : n(n_) {
+    cmax = std::min<size_t>(n, (size_t)1 << 21);
+    // up to 2^24 points: at least 8 chunks, so that copies overlap kernels at all
+    if (n > 2 * kMin) cmax = std::min(cmax, std::max(kMin, ((n + 7) / 8 + 255) & ~(size_t)255));
+    // a streaming consumer (the output digest) starts on the first chunk's records: 2^16 points
+    first = (small_first && n > cmax) ? std::min<size_t>(cmax, (size_t)1 << 16) : cmax;
+    if (cmax < 2 * kMin) return;  // no room for a ramp (calls below ~2^21 points)
+    for (size_t x = kMin; x < cmax; x *= 4) up++, sum_up += x;
+    for (size_t x = kMin; 2 * x <= cmax; x *= 2) down++;  // down: kMin 2^(down-1), ..., 2 kMin, kMin
+    const size_t sum_down = kMin * (((size_t)1 << down) - 1);
+    if (n <= sum_up + sum_down + cmax) return;  // too short: equal chunks
+    ramp = true;
+    rest = n - sum_up - sum_down;
+    mid = (rest + cmax - 1) / cmax;
+  }
+  size_t count() const {
+    if (ramp) return up + mid + down;
+    return first >= n ? 1 : 1 + (n - first + cmax - 1) / cmax;
+  }
+  void span(size_t j, size_t& off, size_t& m) const {  // chunk j = points [off, off + m)
+    if (!ramp) {
+      off = j == 0 ? 0 : first + (j - 1) * cmax;
+      m = std::min(j == 0 ? first : cmax, n - off);
+    } else if (j < up) {
+      off = kMin * ((((size_t)1 << (2 * j)) - 1) / 3);
+      m = kMin << (2 * j);
+    } else if (j < up + mid) {
+      off = sum_up + (j - up) * cmax;
+      m = std::min(cmax, sum_up + rest - off);
+    } else {
+      const size_t k = j - up - mid;
+      off = sum_up + rest + kMin * (((size_t)1 << down) - ((size_t)1 << (down - k)));
+      m = kMin << (down - 1 - k);
+    }
+  }
+  size_t max_chunk() const { return cmax; }
+};
+
 // Run one op over host buffers on device `dev`, in chunks that bound the staging memory. Chunks
 // alternate between two slots/streams: while the GPU decodes chunk k, this thread copies chunk
 // k-1's output out and chunk k+1's input in (pageable copies block the host, not the other
@@ -244,20 +294,13 @@ int run_host(int dev, CodecOp op, const uint8_t* in, size_t n, uint8_t* out, uin
   HIP_TRY(hipSetDevice(dev));
   const uint64_t rin = in_record(op), rout = out_record(op);
   // 2 x 2^21 x 288 B of staging at most. A call of up to 2^24 points is cut into at least 8 chunks
-  // (multiples of the 256-point block, at least 2^17 points = one full wave of blocks on 256 CUs)
-  // so that its PCIe copies overlap its kernels: only the first H2D and the last D2H stay exposed
-  // (2^20 G2 points in one chunk: 31 % over the device-resident time, profiles/r04a_bench_n1.json)
-  size_t chunk = std::min<size_t>(n, (size_t)1 << 21);
-  if (n > ((size_t)2 << 17)) chunk = std::min(chunk, std::max<size_t>((size_t)1 << 17, ((n + 7) / 8 + 255) & ~(size_t)255));
-  // A streaming consumer (on_chunk: the output digest of the e2e pipeline) can only start on the
-  // first chunk's records, so that chunk is small (2^16 points: one ~2 ms wave of blocks) and the
-  // digest starts ~15 ms earlier; the others keep `chunk`.
-  const size_t first = (on_chunk && n > chunk) ? std::min<size_t>(chunk, (size_t)1 << 16) : chunk;
-  const size_t nchunks = first >= n ? 1 : 1 + (n - first + chunk - 1) / chunk;
-  auto span = [&](size_t j, size_t& off, size_t& m) {  // chunk j = points [off, off + m)
-    off = j == 0 ? 0 : first + (j - 1) * chunk;
-    m = std::min(j == 0 ? first : chunk, n - off);
-  };
+  // so that its PCIe copies overlap its kernels (2^20 G2 points in one chunk: 31 % over the
+  // device-resident time, profiles/r04a_bench_n1.json); longer calls ramp their chunk sizes up and
+  // down (ChunkPlan). A streaming consumer (on_chunk: the output digest of the e2e pipeline) can
+  // only start on the first chunk's records, so an equal-chunk call gives it a 2^16-point first chunk.
+  const ChunkPlan plan(n, on_chunk != nullptr);
+  const size_t chunk = plan.max_chunk(), nchunks = plan.count();
+  auto span = [&](size_t j, size_t& off, size_t& m) { plan.span(j, off, m); };
   for (int k = 0; k < (nchunks > 1 ? 2 : 1); k++) {
     Slot& sl = c.slot[k];
     if (!sl.stream) HIP_TRY(hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking));
@@ -1094,6 +1137,20 @@ const char* kzgpot_version(void) { return "kzgpot 0.1.0 (gfx950)"; }
 
 #ifdef KZGPOT_TEST_HOOKS
 // test build only (tests/kzgpot_test_hooks.h)
+// The chunk plan of a host-buffer call of n points (run_host): writes up to cap (offset, count)
+// pairs and returns the number of chunks (tests/test_host.py checks the tiling on the CPU).
+long kzgpot_test_chunk_plan(uint64_t n, int streaming_consumer, uint64_t* spans, long cap) {
+  if (n == 0) return 0;
+  const ChunkPlan plan((size_t)n, streaming_consumer != 0);
+  const long k = (long)plan.count();
+  for (long j = 0; j < k && j < cap; j++) {
+    size_t off, m;
+    plan.span((size_t)j, off, m);
+    spans[2 * j] = off;
+    spans[2 * j + 1] = m;
+  }
+  return k;
+}
 int kzgpot_test_inject_host_fault(int site, long skip) {
   if (site < 0 || site > kFaultHostBuf || skip < 0) return KZGPOT_E_INVALID_ARG;
   g_fault_site = 0;

@@ -30,6 +30,10 @@ int kzgpot_comm_inject_fault(void* comm, int site, uint32_t at);
 #define KZGPOT_HOST_FAULT_THREAD 1
 #define KZGPOT_HOST_FAULT_HOSTBUF 2
 int kzgpot_test_inject_host_fault(int site, long skip);
+/* The chunk plan of a host-buffer call of n points (csrc/capi.hip ChunkPlan): up to cap (offset,
+ * count) pairs into spans; returns the number of chunks. streaming_consumer: the e2e output digest
+ * reads the chunks as they land (its first chunk is small). */
+long kzgpot_test_chunk_plan(uint64_t n, int streaming_consumer, uint64_t* spans, long cap);
 #ifdef __cplusplus
 }
 #endif

@@ -118,12 +118,15 @@ def test_chunked_host_path_first_bad(gpu, oracle_lib):
     assert r.out[:4096 * 96] == ark and r.out[bad_at * 96:(bad_at + 1) * 96] == bytes(96)
 
 
-@pytest.mark.parametrize("n", [(1 << 18), (1 << 18) + 1, 3 * (1 << 17) + 5, (1 << 24) + 3])
+@pytest.mark.parametrize("n", [(1 << 18), (1 << 18) + 1, 3 * (1 << 17) + 5, (1 << 21) + 777, (1 << 24) + 3])
 def test_host_chunk_schedule_boundaries(gpu, oracle_lib, n):
-    """run_host's chunk schedule (csrc/capi.hip): up to 2^18 points one chunk; above, >= 8 chunks of
-    >= 2^17 points (multiples of 256) up to 2^21 — here 1, 3, 4 and 9 chunks, the last a ragged
-    1 / 5 / 3 points. A bad point in the middle and one in the very last record: first_bad is the
-    middle one, each status lands at its global index, every other record is the oracle's."""
+    """run_host's chunk plan (csrc/capi.hip ChunkPlan; its tiling is checked on the CPU by
+    tests/test_host.py): up to 2^18 points one chunk; above, equal chunks of >= 2^17 points — here
+    1, 3 and 4 chunks, the last a ragged 1 / 5 points — and from ~2^21 points a ramp: 2^17 points
+    growing x4 to the chunk size, then halving back to 2^17, the ragged remainder in the middle
+    (2^21 + 777 and 2^24 + 3 points: 10 and 21 chunks). A bad point in the middle and one in the
+    very last record: first_bad is the middle one, each status lands at its global index, every
+    other record is the oracle's."""
     base, ark = _random_stream(oracle_lib, 4096, seed=11)
     reps = -(-n // 4096)
     data = bytearray((base * reps)[:n * 48])

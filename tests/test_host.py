@@ -195,3 +195,43 @@ def test_load_phase1_short_file_is_size_error(kzgpot_mod):
     with pytest.raises(kzgpot_mod.KzgPotError) as e:
         kzgpot_mod.load_phase1_buffer(b"\0" * 100, 3)
     assert e.value.code == -103
+
+
+@pytest.mark.parametrize("streaming", [0, 1], ids=["plain", "digest_consumer"])
+def test_host_chunk_plan_tiles_the_call(kzgpot_mod, streaming):
+    """run_host's chunk plan (csrc/capi.hip ChunkPlan, through the test build's
+    kzgpot_test_chunk_plan): the chunks tile [0, n) in order with no gap or overlap, none exceeds
+    the staging size (2^21 points), calls of 2^20 to 2^24 points get at least 8 chunks, and a long
+    call starts and ends on 2^17-point chunks (so only those chunks' copies are exposed), ramping
+    x4 up and /2 down."""
+    from kzgpot import _lib
+
+    if not os.path.exists(_lib.TEST_LIB_PATH):
+        subprocess.run(["make", "-C", PKG, "-j", "8"], check=True)
+    lib = ctypes.CDLL(_lib.TEST_LIB_PATH)
+    fn = lib.kzgpot_test_chunk_plan
+    fn.restype = ctypes.c_long
+    fn.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64), ctypes.c_long]
+    kmin, cmax_all = 1 << 17, 1 << 21
+    sizes = [1, 255, 256, 1 << 16, (1 << 17) + 1, 1 << 18, (1 << 18) + 1, (1 << 20) + 12345, 1 << 21,
+             (1 << 21) + 7, 3 << 20, (1 << 22) + 999, 1 << 23, (1 << 24) + 3, 1 << 25, (1 << 27) + 5, 1 << 28]
+    for n in sizes:
+        cap = 4096
+        buf = (ctypes.c_uint64 * (2 * cap))()
+        k = fn(n, streaming, buf, cap)
+        assert 0 < k <= cap, (n, k)
+        spans = [(buf[2 * j], buf[2 * j + 1]) for j in range(k)]
+        off = 0
+        for o, m in spans:
+            assert o == off and 0 < m <= cmax_all, (n, spans)
+            off += m
+        assert off == n, (n, off)
+        ms = [m for _, m in spans]
+        if 1 << 20 <= n <= 1 << 24:
+            assert k >= 8, (n, k)
+        if n >= 1 << 23:  # long enough for both ramps
+            assert ms[0] == kmin and ms[-1] == kmin and ms[1] == 4 * kmin, (n, ms[:3], ms[-3:])
+            assert ms[-2] == 2 * kmin, (n, ms[-3:])
+            assert max(ms) == min(cmax_all, max(kmin, ((n + 7) // 8 + 255) & ~255)), (n, max(ms))
+        if streaming and k > 1 and n < 1 << 21:  # equal-chunk calls: a small first chunk for the digest
+            assert ms[0] <= 1 << 16, (n, ms[0])
