@@ -704,7 +704,8 @@ def host_api_rows(seed, dev, D, g1_log2=25, g2_log2=20):
     """The FFI boundary the Rust caller binds (include/kzgpot.h): kzgpot_g1_decompress /
     kzgpot_g2_decompress on PAGEABLE host buffers, as `read_g1` x N is replaced
     (src/lib.rs:41-80, preprocess-kgz.rs:140-153), timed around the C call: PCIe both ways
-    included (run_host pipelines 2^21-point chunks over two streams). Beside each, the same points
+    included (run_host pipelines chunks of up to 2^21 points over two streams, ramping from and back
+    to 2^17-point chunks at both ends of a long call: csrc/capi.hip ChunkPlan). Beside each, the same points
     device-resident (the `_dev` launch, event-timed), so the PCIe overhead is explicit. The first
     call sizes the staging and faults the output pages in; the steady-state call is the row."""
     import numpy as np
