@@ -230,17 +230,30 @@ int decode_key(uint64_t key, int64_t* first_bad) {
 // 2^17-point chunks instead of cmax-point ones (2^25 G1 points: 100 + 201 MB at cmax = 2^21). A
 // call too short for both ramps keeps equal chunks. Chunks are multiples of 256 points but one.
 struct ChunkPlan {
-  size_t n = 0, cmax = 0, first = 0;  // equal-chunk plan: [first, cmax, cmax, ..., tail]
+  size_t n = 0, cmax = 0, first = 0, last = 0;  // equal-chunk plan: [first, cmax, ..., ragged, last]
   bool ramp = false;
   size_t up = 0, mid = 0, down = 0, sum_up = 0, rest = 0;  // ramp plan: up x4, mid x cmax, down /2
-  static constexpr size_t kMin = (size_t)1 << 17;
+#ifndef KZGPOT_CHUNK_END_LOG2  // build knobs for chunk-plan experiments (tools/ab_host_plans.sh)
+#define KZGPOT_CHUNK_END_LOG2 17
+#endif
+#ifndef KZGPOT_CHUNK_FLOOR_LOG2
+#define KZGPOT_CHUNK_FLOOR_LOG2 17
+#endif
+  static constexpr size_t kMin = (size_t)1 << KZGPOT_CHUNK_END_LOG2;      // the ramps' end chunks
+  static constexpr size_t kFloor = (size_t)1 << KZGPOT_CHUNK_FLOOR_LOG2;  // the smallest cmax
   ChunkPlan(size_t n_, bool small_first) : n(n_) {
     cmax = std::min<size_t>(n, (size_t)1 << 21);
     // up to 2^24 points: at least 8 chunks, so that copies overlap kernels at all
-    if (n > 2 * kMin) cmax = std::min(cmax, std::max(kMin, ((n + 7) / 8 + 255) & ~(size_t)255));
+    if (n > 2 * kFloor) cmax = std::min(cmax, std::max(kFloor, ((n + 7) / 8 + 255) & ~(size_t)255));
     // a streaming consumer (the output digest) starts on the first chunk's records: 2^16 points
     first = (small_first && n > cmax) ? std::min<size_t>(cmax, (size_t)1 << 16) : cmax;
-    if (cmax < 2 * kMin) return;  // no room for a ramp (calls below ~2^21 points)
+    if (cmax < 2 * kMin) {  // no room for a ramp (calls below ~2^21 points)
+      // half-size end chunks shorten the exposed first input and last output copies there: 2^20
+      // G2 / G1 points 12.7-13.9 / 14.4-16.4 % over device-resident against 16.0-16.3 / 18.1-18.6 %
+      // with equal chunks, same box (profiles/r06za_ab_plans, variants A and old)
+      if (n > 2 * kMin && cmax == kMin) first = last = kMin / 2;
+      return;
+    }
     for (size_t x = kMin; x < cmax; x *= 4) up++, sum_up += x;
     for (size_t x = kMin; 2 * x <= cmax; x *= 2) down++;  // down: kMin 2^(down-1), ..., 2 kMin, kMin
     const size_t sum_down = kMin * (((size_t)1 << down) - 1);
@@ -251,12 +264,16 @@ struct ChunkPlan {
   }
   size_t count() const {
     if (ramp) return up + mid + down;
-    return first >= n ? 1 : 1 + (n - first + cmax - 1) / cmax;
+    return first >= n ? 1 : 1 + (n - first - last + cmax - 1) / cmax + (last ? 1 : 0);
   }
   void span(size_t j, size_t& off, size_t& m) const {  // chunk j = points [off, off + m)
     if (!ramp) {
+      if (last && j + 1 == count()) {
+        off = n - last, m = last;
+        return;
+      }
       off = j == 0 ? 0 : first + (j - 1) * cmax;
-      m = std::min(j == 0 ? first : cmax, n - off);
+      m = std::min(j == 0 ? first : cmax, n - last - off);
     } else if (j < up) {
       off = kMin * ((((size_t)1 << (2 * j)) - 1) / 3);
       m = kMin << (2 * j);

@@ -235,3 +235,5 @@ def test_host_chunk_plan_tiles_the_call(kzgpot_mod, streaming):
             assert max(ms) == min(cmax_all, max(kmin, ((n + 7) // 8 + 255) & ~255)), (n, max(ms))
         if streaming and k > 1 and n < 1 << 21:  # equal-chunk calls: a small first chunk for the digest
             assert ms[0] <= 1 << 16, (n, ms[0])
+        if 2 * kmin < n <= 8 * kmin:  # equal 2^17-point chunks between 2^16-point end chunks
+            assert ms[0] == ms[-1] == 1 << 16 and max(ms) == kmin, (n, ms)

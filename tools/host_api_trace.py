@@ -1,5 +1,5 @@
 """The host-buffer entry point under a trace (where does the FFI boundary's PCIe overhead go?):
-kzgpot_g1_decompress on 2^`--log2` pageable G1 points, called twice (the first sizes the staging
+kzgpot_g1_decompress (or `--kind g2`) on 2^`--log2` pageable points, called twice (the first sizes the staging
 and faults the output in), as bench.py's host_api row does. Run it under
     rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d DIR -o run -- python3 tools/host_api_trace.py
 and summarise with `--summarise DIR`: the codec kernels' busy union and gaps over the timed call,
@@ -19,7 +19,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "kzg-setup-powersoftau_amd"))
 
 
-def run(log2):
+def run(log2, kind):
     import numpy as np
     import torch
 
@@ -28,32 +28,35 @@ def run(log2):
 
     dev = torch.device("cuda", 0)
     n = 1 << log2
-    comp, _ = D.synth("g1", 7, 0, n, dev, with_expected=False)
+    rout = 96 if kind == "g1" else 192
+    comp, _ = D.synth(kind, 7, 0, n, dev, with_expected=False)
     host_in = comp.cpu().numpy()
     torch.cuda.synchronize()
     lib = _lib.load()
-    out = np.empty(n * 96, np.uint8)
+    out = np.empty(n * rout, np.uint8)
+    call = lib.kzgpot_g1_decompress if kind == "g1" else lib.kzgpot_g2_decompress
     fb = ctypes.c_int64()
     res = {}
     for name in ("first", "timed"):
         out[:] = 0
         t0 = time.time_ns()
-        rc = lib.kzgpot_g1_decompress(host_in.ctypes.data, ctypes.c_size_t(n), out.ctypes.data, 0, ctypes.byref(fb))
+        rc = call(host_in.ctypes.data, ctypes.c_size_t(n), out.ctypes.data, 0, ctypes.byref(fb))
         t1 = time.time_ns()
         res[name] = {"rc": rc, "first_bad": fb.value, "ms": (t1 - t0) / 1e6, "t0_ns": t0, "t1_ns": t1}
         time.sleep(0.2)  # separates the calls in the trace
     # the same points device-resident (bench.py host_api_rows' comparison), event-timed
-    d_out = torch.empty(n * 96, dtype=torch.uint8, device=dev)
+    d_out = torch.empty(n * rout, dtype=torch.uint8, device=dev)
     key = torch.empty(1, dtype=torch.int64, device=dev)
-    D.codec_dev("g1_decompress", comp, d_out, key)
+    D.codec_dev(f"{kind}_decompress", comp, d_out, key)
     e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     e[0].record()
-    D.codec_dev("g1_decompress", comp, d_out, key)
+    D.codec_dev(f"{kind}_decompress", comp, d_out, key)
     e[1].record()
     torch.cuda.synchronize()
     res["device_resident_ms"] = e[0].elapsed_time(e[1])
     res["overhead_frac"] = res["timed"]["ms"] / res["device_resident_ms"] - 1
     res["lib"] = _lib.LIB_PATH
+    res["kind"], res["points"] = kind, n
     print(json.dumps(res))
 
 
@@ -100,9 +103,10 @@ def summarise(d):
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--log2", type=int, default=25)
+    ap.add_argument("--kind", choices=["g1", "g2"], default="g1")
     ap.add_argument("--summarise")
     a = ap.parse_args()
     if a.summarise:
         summarise(a.summarise)
     else:
-        run(a.log2)
+        run(a.log2, a.kind)
